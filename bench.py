@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident block-signature indexing on MI355X.
+
+Metric (BASELINE.json): "GiB/s indexed (device-resident), 4 KiB blocks;
+%HBM peak at 1/2/4/8 GPU".
+
+Workload (BASELINE.json configs[1]): index one 8 GiB synthetic file in 4 KiB
+blocks on one MI355X.  A step = one pass of the hot path over the whole
+buffer: the SHA-1 kernel over every block (input already resident in HBM) ->
+20-byte digest table.  With --gpus N (torchrun, one rank per GPU) the logical
+file is N x 8 GiB, each rank holds its contiguous 8 GiB shard (weak scaling,
+the shard layout of configs[3]) and a step also gathers every shard's digest
+table to rank 0 over RCCL (the exchange the single-file blocks_hash needs).
+
+Also: --config 3 (1024 x 8 MiB files, per-file blocks_hash on device) and
+--config 5 (32 GiB, 64 KiB blocks).
+
+Rank 0 prints ONE JSON line (contract in the task statement), with:
+  roofline      -- the SHA-1 kernel's algorithmic bytes / its average launch
+                   time (HIP events on the launch stream) vs 8.0 TB/s HBM peak;
+                   traffic = HBM bytes per launch from rocprofv3 PMC counters
+                   (profiles/, measured separately) or null;
+  cpu_baseline  -- the C oracle (single-threaded SHA-1 port of the
+                   reference loop) on a bounded sample of the same bytes, rank 0
+                   at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from syncfast_amd import device, host  # noqa: E402
+
+GiB = 1 << 30
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+SEED = 0x5EED0000
+
+CONFIGS = {
+    2: dict(workload="index one 8 GiB synthetic file, 4 KiB blocks (BASELINE configs[1])",
+            bytes=8 * GiB, block=4096, files=1),
+    3: dict(workload="index 1024 x 8 MiB synthetic files, 4 KiB blocks (BASELINE configs[2])",
+            bytes=1024 * 8 * (1 << 20), block=4096, files=1024),
+    5: dict(workload="index one 32 GiB synthetic file, 64 KiB blocks (BASELINE configs[4])",
+            bytes=32 * GiB, block=65536, files=1),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    p.add_argument("--shard-gib", type=float, default=None, help="override bytes per rank (GiB)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(nbytes_total, bs, budget_s):
+    """Time the oracle (C, 1 thread) on the leading bytes of the same
+    synthetic stream, in 64 MiB pieces, until the time budget is used."""
+    import numpy as np
+    import oracle  # test infrastructure: used here only as the timed CPU baseline
+    piece = 64 << 20
+    piece -= piece % bs
+    done = 0
+    t_hash = 0.0
+    while done < nbytes_total and t_hash < budget_s:
+        n = min(piece, nbytes_total - done)
+        buf = oracle.splitmix_bytes(n, SEED, done)  # generation not timed
+        t0 = time.perf_counter()
+        _, _, dig = oracle.index_fixed(buf, bs)
+        t_hash += time.perf_counter() - t0
+        done += n
+        del buf, dig
+    return {"value": round(done / GiB / t_hash, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {done / GiB:.3f} GiB of the same splitmix64 stream, {bs}-B blocks, "
+                      f"oracle/sf_oracle.c SHA-1 (scalar C, no SHA-NI), 1 thread, SQLite excluded"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[a.config]
+    bs = cfg["block"]
+    shard = int(a.shard_gib * GiB) if a.shard_gib else cfg["bytes"]
+    shard -= shard % bs
+    nblk = shard // bs
+
+    # Synthetic input, generated in HBM: rank r holds bytes
+    # [r*shard, (r+1)*shard) of one logical file (seed SEED).
+    data = torch.empty(shard, dtype=torch.uint8, device=dev)
+    device.fill_splitmix(data, SEED, rank * shard)
+    dig = torch.empty((nblk, 20), dtype=torch.uint8, device=dev)
+    files = None
+    if cfg["files"] > 1:
+        flen = shard // cfg["files"]
+        files = [(i * flen, flen) for i in range(cfg["files"])]
+    gathered = None
+    if distributed and not a.no_gather and rank == 0:
+        gathered = [torch.empty_like(dig) for _ in range(world)]
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        if files is None:
+            device.index_device(data, bs, out=dig, stream=stream)
+        else:
+            device.index_device_batch(data, files, bs, file_hashes=True, stream=stream)
+        if i is not None:
+            ev[i][1].record(stream)
+        if distributed and not a.no_gather:
+            dist.gather(dig, gathered if rank == 0 else None, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
+    kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+    t = float(elapsed.item())
+    kern_ms = float(kt.item())
+
+    # Self-check (product host SHA-1): first and last block of this shard.
+    d = dig.cpu().numpy()
+    first = data[:bs].cpu().numpy()
+    lastb = data[(nblk - 1) * bs:].cpu().numpy()
+    assert bytes(d[0]) == host.sha1(first) and bytes(d[-1]) == host.sha1(lastb), "digest self-check failed"
+
+    if rank != 0:
+        if distributed:
+            dist.destroy_process_group()
+        return
+
+    # Host stage of the single-file path: blocks_hash over all digests
+    # (sequential SHA-1, reported separately, not in `value`).
+    bh_ms = None
+    if files is None:
+        full = torch.cat(gathered).cpu().numpy() if gathered else d
+        tb = time.perf_counter()
+        host.blocks_hash(full)
+        bh_ms = (time.perf_counter() - tb) * 1e3
+
+    total_bytes = shard * world
+    gibs = total_bytes / GiB / (t / a.steps)
+    alg_bytes = nblk * (bs + 20)  # read every byte once + write 20 B/block
+    if files is not None:  # + per-file blocks_hash kernel: re-read the digests, write 20 B/file
+        alg_bytes += nblk * 20 + len(files) * 20
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(a.traffic_file) as f:
+            tr = json.load(f)
+        key = f"config{a.config}"
+        if key in tr and tr[key].get("shard_bytes") == shard:
+            traffic = tr[key]["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(shard, bs, a.cpu_seconds)
+
+    line = {
+        "metric": "GiB/s indexed (device-resident), %d KiB blocks" % (bs // 1024),
+        "value": round(gibs, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(t / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 bytes generated in HBM, seed 0x5EED0000)",
+        "config": {"workload": cfg["workload"], "bytes_per_gpu": shard, "block_size": bs,
+                   "total_bytes": total_bytes, "files": cfg["files"], "blocks": nblk * world,
+                   "parallelism": f"shard{world}" + ("+rccl_gather" if distributed and not a.no_gather else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "sha1_fixed_kernel<128>", "kernel_ms": round(kern_ms, 4),
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": cpu,
+        "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+        "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
+    }
+    print(json.dumps(line), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

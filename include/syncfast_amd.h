@@ -1,0 +1,137 @@
+/*
+ * syncfast_amd.h -- C-ABI of the MI355X block-signature indexing path.
+ *
+ * Drop-in boundary for the hot path of syncfast's Index::index_file
+ * (/root/reference/src/index.rs:610-659): file bytes -> one
+ * (offset, size, SHA-1) row per block, plus the per-file blocks_hash
+ * (src/index.rs:661-682).  The reference exposes no FFI of its own; the seam
+ * it replaces is the loop at src/index.rs:621-647 that hands
+ * (HashDigest, offset, size) tuples to Index::add_block (src/index.rs:387-408).
+ * INTEGRATION.md shows the Rust `extern "C"` binding a maintainer would add.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  "d_" pointers are device (HBM) pointers
+ *    on the current HIP device; `stream` is a hipStream_t passed as void*
+ *    (NULL = the null stream).  Device entry points are asynchronous on
+ *    `stream` and may be called from several host threads on different
+ *    streams.
+ *  - Return 0 on success, a negative errno-style SF_E* code otherwise; the
+ *    Rust side maps them to Error::Io (src/lib.rs:25), as the reference
+ *    propagates I/O errors with `?` (src/index.rs:615,630) and exposes no
+ *    partial results.
+ *  - Digests are the 20 bytes of sha1.digest().bytes() (big-endian SHA-1),
+ *    exactly HashDigest's field (src/lib.rs:72-76), stored back to back:
+ *    block i at byte 20*i.
+ *  - Fixed tiling: block i = bytes [i*B, min((i+1)*B, len)).  No empty
+ *    blocks: len == 0 gives 0 blocks, and there is no trailing empty block
+ *    when len % B == 0 (the reference only emits a block on ChunkInput::End
+ *    after data, src/index.rs:629-646).
+ *  - blocks_hash of a file with no blocks is SHA1("") =
+ *    da39a3ee5e6b4b0d3255bfef95601890afd80709.
+ */
+#ifndef SYNCFAST_AMD_H
+#define SYNCFAST_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SF_HASH_DIGEST_LEN 20 /* HASH_DIGEST_LEN, src/lib.rs:72 */
+#define SF_MAX_BLOCK_SIZE (32u << 20) /* fixed-tiling block size limit (32 MiB) */
+
+#define SF_OK 0
+#define SF_EIO (-5)      /* file read failed */
+#define SF_ENOMEM (-12)  /* device / pinned allocation failed */
+#define SF_ENODEV (-19)  /* no HIP device, or a HIP runtime error */
+#define SF_EINVAL (-22)  /* bad argument */
+#define SF_ENOSPC (-28)  /* output capacity too small; *n_out holds the need */
+#define SF_ERANGE (-34)  /* a block lies outside [0, len) */
+
+/* One signature row: what index_file passes to add_block
+ * (src/index.rs:636-642) and what FILE_BLOCK carries on the wire
+ * (src/sync/ssh/proto.rs:162-166).  32 bytes. */
+typedef struct sf_block_sig {
+    uint64_t offset;
+    uint32_t size;
+    uint8_t sha1[SF_HASH_DIGEST_LEN];
+} sf_block_sig;
+
+/* A file inside one device buffer (many-file batch, BASELINE config 3). */
+typedef struct sf_file_desc {
+    uint64_t offset; /* byte offset of the file in the batch buffer */
+    uint64_t len;    /* file length in bytes */
+} sf_file_desc;
+
+/* ------------------------------------------------------------ runtime */
+const char *sf_version(void);
+const char *sf_strerror(int code);
+/* Number of visible HIP devices (0 on a machine without one). */
+int sf_device_count(int *n);
+int sf_set_device(int device);
+
+/* --------------------------------------- device-resident hot path ---- */
+
+/* Fixed tiling of d_data[0, len) into block_size-byte blocks; writes
+ * ceil(len/block_size) digests to d_digests (20 B each).  Replaces the
+ * chunk loop of src/index.rs:621-647 for fixed-size blocks.
+ * SF_ENOSPC (with *n_blocks set) when cap_blocks is too small. */
+int sf_index_device_fixed(const void *d_data, uint64_t len, uint32_t block_size,
+                          void *d_digests, uint64_t cap_blocks, uint64_t *n_blocks,
+                          void *stream);
+
+/* Explicit block list: block i = d_data[d_offsets[i], d_offsets[i] + d_sizes[i]).
+ * Used for content-defined boundaries (src/index.rs:622-625 produces them
+ * in the reference), the reference KAT boundaries and ragged batches.
+ * Blocks need not be sorted, aligned or disjoint.  A block outside
+ * [0, len) is not read: its digest is zeroed and, if d_status != NULL,
+ * *d_status (device int32, caller-initialised to 0) is set to SF_ERANGE. */
+int sf_index_device_blocks(const void *d_data, uint64_t len, const uint64_t *d_offsets,
+                           const uint32_t *d_sizes, uint64_t n_blocks, void *d_digests,
+                           int *d_status, void *stream);
+
+/* Many-file batch: files[] (host array) describes n_files files inside
+ * d_data[0, len).  Writes every file's fixed-size block digests, file after
+ * file, to d_digests (cap_blocks rows) and, if d_file_hashes != NULL, each
+ * file's blocks_hash (20 B per file, src/index.rs:661-682) computed on the
+ * device.  first_block (host, n_files+1 entries, may be NULL) receives the
+ * index of each file's first digest row; *n_blocks the total.  Synchronous
+ * w.r.t. the host for its small block-table upload only. */
+int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *files,
+                          uint32_t n_files, uint32_t block_size, void *d_digests,
+                          uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
+                          uint64_t *n_blocks, void *stream);
+
+/* Deterministic synthetic input (bench / tests): bytes [start, start+len)
+ * of the splitmix64 stream with this seed. */
+int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t start, void *stream);
+
+/* ------------------------------------------------ host-memory entries */
+
+/* End to end from host memory: H2D in pipelined chunks, fixed-tiling kernel,
+ * D2H of the signature rows.  Blocking.  out has cap rows. */
+int sf_index_buffer(const uint8_t *data, uint64_t len, uint32_t block_size,
+                    sf_block_sig *out, uint64_t cap, uint64_t *n_out);
+
+/* End to end from a file on disk (the reference's input, src/index.rs:615):
+ * pread into pinned buffers, overlapped H2D + kernel, D2H.  Writes the
+ * rows and the file's blocks_hash.  Blocking. */
+int sf_index_file(const char *path, uint32_t block_size, sf_block_sig *out, uint64_t cap,
+                  uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
+/* compute_blocks_hash (src/index.rs:661-682) on the host: SHA-1 over the
+ * n 20-byte digests in order.  Sequential by definition; runs on a host
+ * core (SHA-NI when the CPU has it). */
+int sf_blocks_hash(const uint8_t *digests, uint64_t n, uint8_t out[SF_HASH_DIGEST_LEN]);
+int sf_blocks_hash_sigs(const sf_block_sig *sigs, uint64_t n, uint8_t out[SF_HASH_DIGEST_LEN]);
+
+/* Host SHA-1 of an arbitrary byte range (the same function as the
+ * reference's sha1 crate; used for blocks_hash and host-side checks). */
+int sf_sha1_host(const uint8_t *data, uint64_t len, uint8_t out[SF_HASH_DIGEST_LEN]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYNCFAST_AMD_H */

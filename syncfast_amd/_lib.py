@@ -1,0 +1,110 @@
+"""ctypes binding of libsyncfast_amd.so (the C-ABI in include/syncfast_amd.h).
+
+The library is built in-tree (``syncfast_amd/lib/libsyncfast_amd.so``) by
+``__graft_entry__.build()`` / ``make -C syncfast_amd/csrc``.  There is no
+Python or CPU fallback: if the library is missing, importing the compute
+entry points raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsyncfast_amd.so")
+
+SF_OK = 0
+SF_EIO = -5
+SF_ENOMEM = -12
+SF_ENODEV = -19
+SF_EINVAL = -22
+SF_ENOSPC = -28
+SF_ERANGE = -34
+
+HASH_DIGEST_LEN = 20
+MAX_BLOCK_SIZE = 32 << 20
+
+# Every symbol include/syncfast_amd.h declares (checked by the CPU tests).
+EXPORTED = (
+    "sf_version", "sf_strerror", "sf_device_count", "sf_set_device",
+    "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
+    "sf_fill_splitmix_device", "sf_index_buffer", "sf_index_file",
+    "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
+)
+
+
+class SfError(OSError):
+    """A negative SF_E* return code (maps to the reference's Error::Io)."""
+
+    def __init__(self, code: int, what: str = ""):
+        msg = _strerror(code)
+        super().__init__(-code, f"{what}: {msg}" if what else msg)
+        self.code = code
+
+
+class BlockSig(ctypes.Structure):
+    """sf_block_sig: (offset, size, sha1[20]) -- 32 bytes."""
+    _fields_ = [("offset", ctypes.c_uint64), ("size", ctypes.c_uint32),
+                ("sha1", ctypes.c_uint8 * 20)]
+
+
+class FileDesc(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("len", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    L.sf_version.restype = ctypes.c_char_p
+    L.sf_version.argtypes = []
+    L.sf_strerror.restype = ctypes.c_char_p
+    L.sf_strerror.argtypes = [i32]
+    L.sf_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.sf_set_device.argtypes = [i32]
+    L.sf_index_device_fixed.argtypes = [vp, u64, u32, vp, u64, pu64, vp]
+    L.sf_index_device_blocks.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp]
+    L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp]
+    L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
+    L.sf_index_buffer.argtypes = [vp, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
+    L.sf_index_file.argtypes = [ctypes.c_char_p, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
+    L.sf_blocks_hash.argtypes = [vp, u64, vp]
+    L.sf_blocks_hash_sigs.argtypes = [ctypes.POINTER(BlockSig), u64, vp]
+    L.sf_sha1_host.argtypes = [vp, u64, vp]
+    for name in EXPORTED:
+        if name not in ("sf_version", "sf_strerror"):
+            getattr(L, name).restype = ctypes.c_int
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(syncfast_amd has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _strerror(code: int) -> str:
+    try:
+        return lib().sf_strerror(code).decode()
+    except ImportError:
+        return f"error {code}"
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != SF_OK:
+        raise SfError(rc, what)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib().sf_device_count(ctypes.byref(n)), "sf_device_count")
+    return n.value

@@ -1,0 +1,354 @@
+// sf_capi.hip -- the C-ABI (include/syncfast_amd.h) over the gfx950 kernels.
+//
+// Every entry point here is a host function with plain pointers/sizes; the
+// compute happens in the kernels of sf_kernels.hpp.  There is no CPU
+// implementation of the block hashing in this library: without a HIP device
+// the device entry points return SF_ENODEV.
+#include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/syncfast_amd.h"
+#include "sf_kernels.hpp"
+
+extern "C" void sf_host_sha1_impl(const uint8_t* data, uint64_t len, uint8_t out[20], int force_scalar);
+
+namespace {
+
+constexpr int kTile = 128;  // bytes of each block staged per LDS step
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int hip_err(hipError_t e) {
+  if (e == hipSuccess) return SF_OK;
+  if (e == hipErrorOutOfMemory) return SF_ENOMEM;
+  return SF_ENODEV;
+}
+
+#define SF_HIP(call)                       \
+  do {                                     \
+    hipError_t _e = (call);                \
+    if (_e != hipSuccess) return hip_err(_e); \
+  } while (0)
+
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+inline unsigned grid_for_blocks(uint64_t nblocks) {
+  const uint64_t waves = ceil_div(nblocks, 64);
+  return (unsigned)ceil_div(waves, sf::kWavesPerWG);
+}
+
+int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
+                 hipStream_t stream) {
+  if (nblocks == 0) return SF_OK;
+  const unsigned grid = grid_for_blocks(nblocks);
+  hipLaunchKernelGGL(sf::sha1_fixed_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
+                     static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests));
+  return hip_err(hipGetLastError());
+}
+
+int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
+                 uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream) {
+  if (nblocks == 0) return SF_OK;
+  const unsigned grid = grid_for_blocks(nblocks);
+  hipLaunchKernelGGL(sf::sha1_table_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
+                     static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
+                     static_cast<uint8_t*>(d_digests), d_status);
+  return hip_err(hipGetLastError());
+}
+
+int check_fixed_args(uint64_t len, uint32_t bs) {
+  if (bs == 0 || bs > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
+  (void)len;
+  return SF_OK;
+}
+
+// RAII device / pinned allocations for the host-memory entry points.
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+struct PinBuf {
+  void* p = nullptr;
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+struct Streams {
+  hipStream_t s[2] = {nullptr, nullptr};
+  ~Streams() {
+    for (auto x : s)
+      if (x) (void)hipStreamDestroy(x);
+  }
+};
+
+// Chunk of input handled per pipeline stage: a whole number of blocks, about
+// 256 MiB.
+inline uint64_t stage_bytes(uint32_t bs) {
+  const uint64_t target = 256ull << 20;
+  const uint64_t nb = std::max<uint64_t>(1, target / bs);
+  return nb * bs;
+}
+
+// Shared driver of sf_index_buffer / sf_index_file: `read(dst, off, n)`
+// fills a pinned staging buffer with input bytes [off, off+n).
+template <typename ReadFn>
+int index_pipelined(uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap, uint64_t* n_out, ReadFn read) {
+  const uint64_t nblocks = len ? ceil_div(len, bs) : 0;
+  if (n_out) *n_out = nblocks;
+  if (nblocks > cap) return SF_ENOSPC;
+  if (nblocks == 0) return SF_OK;
+  const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
+  const uint64_t nstages = ceil_div(len, stage);
+  Streams st;
+  DevBuf ddata[2], ddig;
+  PinBuf pin[2], pdig;
+  for (int i = 0; i < 2; i++) {
+    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
+    SF_HIP(hipMalloc(&ddata[i].p, stage));
+    SF_HIP(hipHostMalloc(&pin[i].p, stage, hipHostMallocDefault));
+  }
+  SF_HIP(hipMalloc(&ddig.p, nblocks * 20));
+  SF_HIP(hipHostMalloc(&pdig.p, nblocks * 20, hipHostMallocDefault));
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  int rc = SF_OK;
+  for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    const uint64_t off = k * stage;
+    const uint64_t n = std::min(stage, len - off);
+    if (k >= 2) {
+      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    }
+    rc = read(static_cast<uint8_t*>(pin[b].p), off, n);
+    if (rc != SF_OK) break;
+    if (hipMemcpyAsync(ddata[b].p, pin[b].p, n, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    const uint64_t first_blk = off / bs;
+    const uint64_t nb = ceil_div(n, bs);
+    rc = launch_fixed(ddata[b].p, n, bs, nb, static_cast<uint8_t*>(ddig.p) + first_blk * 20, st.s[b]);
+    if (rc != SF_OK) break;
+    if (hipEventRecord(done[b], st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+  }
+  for (int i = 0; i < 2; i++) {
+    if (hipStreamSynchronize(st.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+    (void)hipEventDestroy(done[i]);
+  }
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
+  for (uint64_t i = 0; i < nblocks; i++) {
+    out[i].offset = i * bs;
+    out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
+    memcpy(out[i].sha1, dg + 20 * i, 20);
+  }
+  return SF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sf_version(void) { return "syncfast_amd 0.1.0 (gfx950)"; }
+
+const char* sf_strerror(int code) {
+  switch (code) {
+    case SF_OK: return "ok";
+    case SF_EIO: return "I/O error";
+    case SF_ENOMEM: return "out of memory";
+    case SF_ENODEV: return "no HIP device or HIP runtime error";
+    case SF_EINVAL: return "invalid argument";
+    case SF_ENOSPC: return "output capacity too small";
+    case SF_ERANGE: return "block outside the input";
+    default: return "unknown error";
+  }
+}
+
+int sf_device_count(int* n) {
+  if (!n) return SF_EINVAL;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return SF_OK;
+}
+
+int sf_set_device(int device) { return hip_err(hipSetDevice(device)); }
+
+int sf_index_device_fixed(const void* d_data, uint64_t len, uint32_t block_size, void* d_digests,
+                          uint64_t cap_blocks, uint64_t* n_blocks, void* stream) {
+  int rc = check_fixed_args(len, block_size);
+  if (rc) return rc;
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_blocks) *n_blocks = nb;
+  if (nb > cap_blocks) return SF_ENOSPC;
+  if (nb && (!d_data || !d_digests)) return SF_EINVAL;
+  return launch_fixed(d_data, len, block_size, nb, d_digests, as_stream(stream));
+}
+
+int sf_index_device_blocks(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
+                           uint64_t n_blocks, void* d_digests, int* d_status, void* stream) {
+  if (n_blocks == 0) return SF_OK;
+  // d_data may be NULL only when len == 0 (then every in-range block is
+  // empty and the kernel dereferences nothing).
+  if (!d_offsets || !d_sizes || !d_digests || (!d_data && len)) return SF_EINVAL;
+  return launch_table(d_data, len, d_offsets, d_sizes, n_blocks, d_digests, d_status, as_stream(stream));
+}
+
+int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,
+                          uint32_t block_size, void* d_digests, uint64_t cap_blocks, void* d_file_hashes,
+                          uint64_t* first_block, uint64_t* n_blocks, void* stream) {
+  int rc = check_fixed_args(len, block_size);
+  if (rc) return rc;
+  if (n_files && !files) return SF_EINVAL;
+  hipStream_t s = as_stream(stream);
+  // Plan: per-file block ranges (host, O(n_files)).
+  std::vector<uint64_t> fb(n_files + 1);
+  uint64_t total = 0;
+  bool contiguous_aligned = true;  // files back to back, every file a whole number of blocks
+  uint64_t expect = files && n_files ? files[0].offset : 0;
+  for (uint32_t f = 0; f < n_files; f++) {
+    if (files[f].offset > len || files[f].len > len - files[f].offset) return SF_ERANGE;
+    fb[f] = total;
+    total += files[f].len ? ceil_div(files[f].len, block_size) : 0;
+    if (files[f].offset != expect || files[f].len % block_size) contiguous_aligned = false;
+    expect = files[f].offset + files[f].len;
+  }
+  fb[n_files] = total;
+  if (first_block) memcpy(first_block, fb.data(), sizeof(uint64_t) * (n_files + 1));
+  if (n_blocks) *n_blocks = total;
+  if (total > cap_blocks) return SF_ENOSPC;
+  if (n_files == 0) return SF_OK;
+  if (!d_data || (total && !d_digests)) return SF_EINVAL;
+
+  // Block table for the ragged case, file table for blocks_hash; one device
+  // workspace, uploaded once.
+  const bool need_table = !contiguous_aligned && total > 0;
+  const bool need_fh = d_file_hashes != nullptr;
+  const size_t tbl_bytes = need_table ? total * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
+  const size_t fh_bytes = need_fh ? (size_t)n_files * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
+  std::vector<uint8_t> host_ws(tbl_bytes + fh_bytes + 16);
+  uint64_t* h_off = reinterpret_cast<uint64_t*>(host_ws.data());
+  uint32_t* h_sz = reinterpret_cast<uint32_t*>(host_ws.data() + total * sizeof(uint64_t) * (need_table ? 1 : 0));
+  if (need_table) {
+    uint64_t i = 0;
+    for (uint32_t f = 0; f < n_files; f++)
+      for (uint64_t o = 0; o < files[f].len; o += block_size, i++) {
+        h_off[i] = files[f].offset + o;
+        h_sz[i] = (uint32_t)std::min<uint64_t>(block_size, files[f].len - o);
+      }
+  }
+  uint64_t* h_foff = reinterpret_cast<uint64_t*>(host_ws.data() + tbl_bytes);
+  uint32_t* h_fsz = reinterpret_cast<uint32_t*>(host_ws.data() + tbl_bytes + (need_fh ? n_files * sizeof(uint64_t) : 0));
+  if (need_fh) {
+    for (uint32_t f = 0; f < n_files; f++) {
+      const uint64_t nbf = fb[f + 1] - fb[f];
+      if (nbf * 20 > 0xFFFFFFFFull) return SF_EINVAL;
+      h_foff[f] = fb[f] * 20;
+      h_fsz[f] = (uint32_t)(nbf * 20);
+    }
+  }
+  DevBuf ws;
+  if (tbl_bytes + fh_bytes) {
+    SF_HIP(hipMalloc(&ws.p, tbl_bytes + fh_bytes));
+    SF_HIP(hipMemcpy(ws.p, host_ws.data(), tbl_bytes + fh_bytes, hipMemcpyHostToDevice));
+  }
+  uint8_t* dws = static_cast<uint8_t*>(ws.p);
+  if (total) {
+    if (contiguous_aligned) {
+      const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
+      rc = launch_fixed(base, fb[n_files] * (uint64_t)block_size, block_size, total, d_digests, s);
+    } else {
+      rc = launch_table(d_data, len, reinterpret_cast<const uint64_t*>(dws),
+                        reinterpret_cast<const uint32_t*>(dws + total * sizeof(uint64_t)), total, d_digests,
+                        nullptr, s);
+    }
+    if (rc) return rc;
+  }
+  if (need_fh) {
+    // blocks_hash of every file at once: one lane per file hashes its own
+    // run of 20-byte digests (a file with no blocks hashes the empty string).
+    const uint8_t* dg = total ? static_cast<const uint8_t*>(d_digests) : static_cast<const uint8_t*>(d_file_hashes);
+    rc = launch_table(dg, total * 20, reinterpret_cast<const uint64_t*>(dws + tbl_bytes),
+                      reinterpret_cast<const uint32_t*>(dws + tbl_bytes + n_files * sizeof(uint64_t)), n_files,
+                      d_file_hashes, nullptr, s);
+    if (rc) return rc;
+  }
+  // The workspace is freed on return: keep the stream ordered before that.
+  SF_HIP(hipStreamSynchronize(s));
+  return SF_OK;
+}
+
+int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t start, void* stream) {
+  if (len == 0) return SF_OK;
+  if (!d_out) return SF_EINVAL;
+  const uint64_t nvec = len / 16 + 1;
+  const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(nvec, 256), 65536);
+  hipLaunchKernelGGL(sf::fill_splitmix_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                     static_cast<uint8_t*>(d_out), len, seed, start);
+  return hip_err(hipGetLastError());
+}
+
+int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
+                    uint64_t* n_out) {
+  int rc = check_fixed_args(len, block_size);
+  if (rc) return rc;
+  if (len && (!data || !out)) return SF_EINVAL;
+  return index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
+    memcpy(dst, data + off, n);
+    return SF_OK;
+  });
+}
+
+int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
+                  uint8_t blocks_hash[20]) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (!path) return SF_EINVAL;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return SF_EIO;
+  const off_t end = lseek(fd, 0, SEEK_END);
+  if (end < 0) { close(fd); return SF_EIO; }
+  const uint64_t len = (uint64_t)end;
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_out) *n_out = nb;
+  if (nb > cap) { close(fd); return SF_ENOSPC; }
+  if (nb && !out) { close(fd); return SF_EINVAL; }
+  rc = index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
+    uint64_t got = 0;
+    while (got < n) {
+      const ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
+      if (r <= 0) return SF_EIO;
+      got += (uint64_t)r;
+    }
+    return SF_OK;
+  });
+  close(fd);
+  if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
+  return rc;
+}
+
+int sf_sha1_host(const uint8_t* data, uint64_t len, uint8_t out[20]) {
+  if (!out || (len && !data)) return SF_EINVAL;
+  sf_host_sha1_impl(data, len, out, 0);
+  return SF_OK;
+}
+
+int sf_blocks_hash(const uint8_t* digests, uint64_t n, uint8_t out[20]) {
+  if (!out || (n && !digests)) return SF_EINVAL;
+  sf_host_sha1_impl(digests, n * 20, out, 0);
+  return SF_OK;
+}
+
+int sf_blocks_hash_sigs(const sf_block_sig* sigs, uint64_t n, uint8_t out[20]) {
+  if (!out || (n && !sigs)) return SF_EINVAL;
+  // Gather the digests into one contiguous run (AoS rows are 32 B apart).
+  std::vector<uint8_t> buf(n * 20);
+  for (uint64_t i = 0; i < n; i++) memcpy(buf.data() + 20 * i, sigs[i].sha1, 20);
+  sf_host_sha1_impl(buf.data(), n * 20, out, 0);
+  return SF_OK;
+}
+
+}  // extern "C"

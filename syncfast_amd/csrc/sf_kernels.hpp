@@ -1,0 +1,329 @@
+// sf_kernels.hpp -- the MI355X block-signature kernels (device code, included by sf_capi.hip).
+//
+// Replaces the hot loop of Index::index_file, /root/reference/src/index.rs:
+// 629-647 (SHA-1 of every block; `Sha1::update` / `digest` / `reset`) and is
+// reused for compute_blocks_hash (src/index.rs:661-682) of many files at once.
+//
+// Design (DESIGN.md "Kernels"):
+//   * one LANE per block: SHA-1 is sequential inside a message, so a block is
+//     a lane's private message and a wave hashes 64 blocks in lockstep;
+//   * a wave's 64 blocks are streamed through a per-wave LDS tile of
+//     64 blocks x TILE bytes, filled by LDS-DMA (`buffer_load_dwordx4 ... lds`):
+//     every DMA wave-instruction moves TILE/16 full 16-B pieces of 1024/TILE
+//     blocks, so each instruction reads whole 128-B lines; the piece order is
+//     XOR-swizzled on the SOURCE address so that the per-lane `ds_read_b128`
+//     of a block's own pieces is bank-conflict free;
+//   * the tile for step t+1 is issued right after step t's words are in
+//     registers, so one DMA per wave is always in flight behind TILE/64
+//     compressions of VALU work;
+//   * the final (padding) chunk(s) of each block are built with per-lane,
+//     bounds-checked loads, so nothing is ever read outside [0, len).
+// Buffer resources carry num_records = bytes left in the wave's span, so a
+// DMA lane past the end reads zeros instead of faulting.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sha1_device.hpp"
+
+namespace sf {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 4;
+constexpr int kThreads = kWave * kWavesPerWG;
+constexpr uint32_t kRsrcWord3 = 0x00020000u;  // raw buffer, gfx9 family
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// ---------------------------------------------------------- wave helpers
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    uint64_t o = __shfl_xor((unsigned long long)v, m, 64);
+    v = o < v ? o : v;
+  }
+  return v;  // identical in every lane
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    uint64_t o = __shfl_xor((unsigned long long)v, m, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+
+// Number of SHA-1 compressions for a message of `size` bytes.
+__device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
+
+// Chunk c (0-based) of the padded message of a block of `size` bytes that
+// starts at p (global memory).  Reads only bytes [0, size) of the block.
+__device__ __forceinline__ void build_tail_chunk(uint32_t (&w)[16], const uint8_t* p, uint32_t size,
+                                                 uint32_t c, uint32_t nch) {
+  const int64_t rem = (int64_t)size - (int64_t)c * 64;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t v = rem - 4 * j;  // valid data bytes in word j
+    uint32_t x = 0;
+    const uint8_t* q = p + (uint64_t)c * 64 + 4 * j;
+    if (v >= 4) {
+      x = bswap32(ld_u32_any(q));
+    } else if (v > 0) {
+      uint32_t y = (uint32_t)q[0] << 24;
+      if (v > 1) y |= (uint32_t)q[1] << 16;
+      if (v > 2) y |= (uint32_t)q[2] << 8;
+      x = y | (0x80u << (8 * (3 - (int)v)));
+    } else if (v == 0) {
+      x = 0x80000000u;
+    }
+    w[j] = x;
+  }
+  if (c == nch - 1) {
+    w[14] = size >> 29;
+    w[15] = size << 3;
+  }
+}
+
+// Per-wave geometry of the blocks handled by this wave.
+struct WaveGeo {
+  uint64_t base;      // byte offset of the wave's span in `data`
+  uint64_t span;      // bytes in [base, end of last block)
+  uint32_t min_size;  // min block size over valid lanes
+  uint32_t max_nch;   // max compressions over valid lanes
+  bool lds_ok;        // 16-B aligned pieces and span < 4 GiB
+};
+
+// Issue the LDS-DMA fill of step `step` (bytes [step*TILE, step*TILE+TILE) of
+// every block) into the wave's tile.  The buffer resource starts at the step
+// and covers the rest of the span, so lanes past the span read zeros.
+template <int TILE>
+__device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t span, uint32_t step,
+                                           const uint32_t (&voff)[TILE / 16], uint4* wave_tile) {
+  const uint64_t toff = (uint64_t)step * TILE;
+  const uint64_t left = span > toff ? span - toff : 0;
+  const uint32_t nrec = left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left;
+  __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(span_ptr + toff), (short)0, (int)nrec, (int)kRsrcWord3);
+#pragma unroll
+  for (int j = 0; j < TILE / 16; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, 0);
+}
+
+// Hash the block (off, size) owned by this lane; all 64 lanes of the wave
+// enter together.  `rel` = off - geo.base (valid lanes).  TILE = bytes of
+// each block staged per LDS step.
+template <int TILE>
+__device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
+                                          uint32_t rel, bool valid, const WaveGeo& geo,
+                                          uint4* __restrict__ wave_tile, Sha1& st) {
+  constexpr int PIECES = TILE / 16;           // 16-B pieces per block per step
+  constexpr int CH = TILE / 64;               // compressions per step
+  constexpr int GSHIFT = PIECES == 4 ? 2 : (PIECES == 8 ? 1 : 0);
+  constexpr int BLK_PER_DMA = 1024 / TILE;    // blocks covered by one DMA wave-instruction
+  static_assert(PIECES == 4 || PIECES == 8 || PIECES == 16, "TILE must be 64, 128 or 256");
+  const int lane = threadIdx.x & 63;
+
+  st.init();
+  const uint32_t nfull = geo.min_size / 64u;
+  uint32_t c_done = 0;
+  if (geo.lds_ok) {
+    const uint32_t nsteps = nfull / CH;
+    // Source offsets (relative to the span base) of this lane's 16-B piece in
+    // each of the PIECES DMA instructions of one step.  Instruction j writes
+    // LDS bytes [j*1024, j*1024+1024): lane -> block b, slot s; slot s holds
+    // piece k = s ^ g(b) so that the reads below are conflict free.
+    uint32_t voff[PIECES];
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      const int b = j * BLK_PER_DMA + lane / PIECES;
+      const int s = lane % PIECES;
+      const int k = s ^ ((b >> GSHIFT) & (PIECES - 1));
+      const uint32_t rel_b = (uint32_t)__shfl((int)rel, b, 64);
+      voff[j] = rel_b + (uint32_t)k * 16u;
+    }
+    const int g = (lane >> GSHIFT) & (PIECES - 1);
+    const uint4* my = wave_tile + lane * PIECES;
+    const uint8_t* span_ptr = data + geo.base;
+
+    if (nsteps > 0) issue_step<TILE>(span_ptr, geo.span, 0, voff, wave_tile);
+    for (uint32_t t = 0; t < nsteps; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint4 raw[PIECES];
+#pragma unroll
+      for (int k = 0; k < PIECES; ++k) raw[k] = my[k ^ g];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 1 < nsteps) issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v = raw[ch * 4 + q];
+          w[4 * q + 0] = bswap32(v.x);
+          w[4 * q + 1] = bswap32(v.y);
+          w[4 * q + 2] = bswap32(v.z);
+          w[4 * q + 3] = bswap32(v.w);
+        }
+        st.compress(w);
+      }
+    }
+    c_done = nsteps * CH;
+  } else {
+    // Misaligned or > 4 GiB span: each lane streams its own block.
+    const uint8_t* p = data + off;
+    for (uint32_t c = 0; c < nfull; ++c) {
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = bswap32(ld_u32_any(p + (uint64_t)c * 64 + 4 * j));
+      st.compress(w);
+    }
+    c_done = nfull;
+  }
+  // Remaining data chunks and the padding chunk(s), per lane.
+  const uint32_t nch = n_chunks(size);
+  for (uint32_t c = c_done; c < geo.max_nch; ++c) {
+    if (valid && c < nch) {
+      uint32_t w[16];
+      build_tail_chunk(w, data + off, size, c, nch);
+      st.compress(w);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+
+// Fixed tiling: block i = data[i*bs, min((i+1)*bs, len)).
+template <int TILE>
+__global__ void __launch_bounds__(kThreads)
+sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
+                  uint8_t* __restrict__ digests) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
+  if (first >= nblocks) return;  // wave-uniform
+  const uint64_t blk = first + lane;
+  const bool valid = blk < nblocks;
+  const uint64_t off = valid ? blk * bs : first * bs;
+  const uint32_t size = valid ? (uint32_t)(len - off < bs ? len - off : bs) : 0u;
+
+  WaveGeo geo;
+  geo.base = first * bs;
+  const uint64_t last = (first + 64 <= nblocks) ? first + 63 : nblocks - 1;
+  geo.span = len - geo.base < (last - first + 1) * (uint64_t)bs ? len - geo.base : (last - first + 1) * (uint64_t)bs;
+  const uint32_t last_size = (uint32_t)(len - last * bs < bs ? len - last * bs : bs);
+  geo.min_size = last_size < bs ? last_size : bs;
+  geo.max_nch = n_chunks(bs);
+  geo.lds_ok = ((bs & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
+               (64ull * bs < 0xF0000000ull);
+  const uint32_t rel = (uint32_t)((uint64_t)lane * bs);
+
+  Sha1 st;
+  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st);
+  if (valid) st.store(digests + blk * 20);
+}
+
+// Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
+// Used for content-defined boundaries, the reference KAT boundaries, ragged
+// many-file batches, and (over the digest table) per-file blocks_hash.
+// A block outside [0, len) is not read: its digest is zeroed and *status is
+// set to -34 (SF_ERANGE).
+template <int TILE>
+__global__ void __launch_bounds__(kThreads)
+sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
+                  const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
+                  int* __restrict__ status) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
+  if (first >= nblocks) return;
+  const uint64_t blk = first + lane;
+  bool valid = blk < nblocks;
+  uint64_t off = 0;
+  uint32_t size = 0;
+  bool bad = false;
+  if (valid) {
+    off = offsets[blk];
+    size = sizes[blk];
+    if (off > len || (uint64_t)size > len - off) {
+      bad = true;
+      off = 0;
+      size = 0;
+    }
+  }
+  WaveGeo geo;
+  const uint64_t lo = wave_min_u64(valid ? off : ~0ull);
+  const uint64_t hi = wave_max_u64(valid ? off + size : 0ull);
+  geo.base = lo;
+  geo.span = hi - lo;
+  geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
+  geo.max_nch = wave_max_u32(valid ? n_chunks(size) : 0u);
+  const bool aligned = !valid || ((off & 15u) == 0);
+  geo.lds_ok = __all(aligned) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
+  const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
+
+  Sha1 st;
+  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st);
+  if (valid) {
+    if (bad) {
+      uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);
+      o[0] = o[1] = o[2] = o[3] = o[4] = 0;
+      if (status) *status = -34;
+    } else {
+      st.store(digests + blk * 20);
+    }
+  }
+}
+
+// splitmix64 byte stream: word i = mix(seed + (i+1)*GAMMA),
+// little-endian; writes bytes [start, start+len) of the stream.
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256)
+fill_splitmix_kernel(uint8_t* __restrict__ out, uint64_t len, uint64_t seed, uint64_t start) {
+  // Fast path: whole 16-B groups of 2 aligned stream words.
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  if ((start & 15u) == 0 && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    const uint64_t nvec = len / 16;
+    const uint64_t w0 = start / 8;
+    for (uint64_t v = tid; v < nvec; v += stride) {
+      const uint64_t a = splitmix_word(seed, w0 + 2 * v), b = splitmix_word(seed, w0 + 2 * v + 1);
+      reinterpret_cast<ulonglong2*>(out)[v] = make_ulonglong2(a, b);
+    }
+    for (uint64_t p = nvec * 16 + tid; p < len; p += stride) {
+      const uint64_t sp = start + p;
+      out[p] = (uint8_t)(splitmix_word(seed, sp >> 3) >> (8 * (sp & 7)));
+    }
+  } else {
+    for (uint64_t p = tid; p < len; p += stride) {
+      const uint64_t sp = start + p;
+      out[p] = (uint8_t)(splitmix_word(seed, sp >> 3) >> (8 * (sp & 7)));
+    }
+  }
+}
+
+
+}  // namespace sf

@@ -1,0 +1,60 @@
+// sha1_device.hpp -- SHA-1 building blocks for gfx950 (one lane = one message).
+//
+// The arithmetic is FIPS 180-4 SHA-1, the function the reference applies per
+// block through the `sha1 0.6.0` crate (/root/reference/src/index.rs:628-644)
+// and over the digest list in compute_blocks_hash (src/index.rs:661-682).
+//
+// Cost model (CDNA4): one 64-byte compression = 80 rounds x 5 VALU
+// (v_alignbit rotl5, v_bitop3 f, 2 x v_add3, v_alignbit rotl30) + 64 x 3
+// schedule ops (v_bitop3 xor3, v_xor, v_alignbit rotl1) + 16 v_perm byte swaps
+// + 5 feed-forward adds ~= 613 VALU per 64 B.  hipcc forms all of these from
+// the plain C++ below (checked in the .s).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sf {
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
+  return __builtin_amdgcn_alignbit(x, x, 32u - n);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct Sha1 {
+  uint32_t h0, h1, h2, h3, h4;
+  __device__ __forceinline__ void init() {
+    h0 = 0x67452301u; h1 = 0xEFCDAB89u; h2 = 0x98BADCFEu; h3 = 0x10325476u; h4 = 0xC3D2E1F0u;
+  }
+  // One compression over 16 big-endian message words (w is clobbered: it
+  // holds the rolling 16-word schedule window).
+  __device__ __forceinline__ void compress(uint32_t (&w)[16]) {
+    uint32_t a = h0, b = h1, c = h2, d = h3, e = h4;
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        wt = rotl(w[(t + 13) & 15] ^ w[(t + 8) & 15] ^ w[(t + 2) & 15] ^ w[t & 15], 1);
+        w[t & 15] = wt;
+      }
+      uint32_t f, k;
+      if (t < 20) { f = d ^ (b & (c ^ d)); k = 0x5A827999u; }
+      else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
+      else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8F1BBCDCu; }
+      else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+      const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
+      e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
+  }
+  // Digest bytes in sha1.digest().bytes() order (big-endian), as 5 words
+  // ready for a little-endian store.
+  __device__ __forceinline__ void store(uint8_t* out20) const {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out20);
+    o[0] = bswap32(h0); o[1] = bswap32(h1); o[2] = bswap32(h2); o[3] = bswap32(h3); o[4] = bswap32(h4);
+  }
+};
+
+}  // namespace sf

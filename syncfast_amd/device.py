@@ -1,0 +1,144 @@
+"""Device-resident entry points over torch tensors (HBM buffers).
+
+PyTorch is only plumbing here: it owns the HBM allocations and the stream.
+Every compute call goes to a HIP kernel through the C-ABI
+(``include/syncfast_amd.h``); tensors must live on a ROCm device.
+
+Reference mapping (/root/reference):
+  index_device          -> the chunk loop of Index::index_file, src/index.rs:621-647
+                           (fixed-size blocks)
+  index_device_blocks   -> the same loop for an explicit boundary list
+                           (the reference's CDC boundaries, src/index.rs:622-625)
+  index_device_batch    -> index_path_rec over many files (src/index.rs:689-715)
+                           + compute_blocks_hash per file (src/index.rs:661-682)
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
+
+__all__ = [
+    "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
+    "fill_splitmix", "splitmix_tensor",
+]
+
+
+def _require_device(t: torch.Tensor, name: str, dtype=None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be on a ROCm device (got {t.device}); syncfast_amd has no CPU path")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _stream_ptr(t: torch.Tensor, stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(t.device)
+    return s.cuda_stream
+
+
+def num_blocks(length: int, block_size: int) -> int:
+    """ceil(len / B); 0 for an empty input (no empty blocks)."""
+    return (length + block_size - 1) // block_size if length else 0
+
+
+def index_device(data: torch.Tensor, block_size: int, out: Optional[torch.Tensor] = None,
+                 stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """SHA-1 of every fixed-size block of a uint8 HBM buffer -> uint8[n, 20]."""
+    _require_device(data, "data", torch.uint8)
+    n = num_blocks(data.numel(), block_size)
+    if out is None:
+        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+    else:
+        _require_device(out, "out", torch.uint8)
+        if out.numel() < 20 * n:
+            raise ValueError(f"out holds {out.numel() // 20} digests, need {n}")
+    nb = ctypes.c_uint64(0)
+    with torch.cuda.device(data.device):
+        check(lib().sf_index_device_fixed(data.data_ptr() if data.numel() else None, data.numel(),
+                                          block_size, out.data_ptr() if n else None, out.numel() // 20,
+                                          ctypes.byref(nb), _stream_ptr(data, stream)),
+              "sf_index_device_fixed")
+    return out
+
+
+def index_device_blocks(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                        out: Optional[torch.Tensor] = None, check_range: bool = True,
+                        stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """SHA-1 of explicit blocks data[offsets[i] : offsets[i] + sizes[i]].
+
+    ``offsets`` int64 and ``sizes`` int32 tensors on the same device.  With
+    ``check_range`` a block outside the buffer raises SfError(SF_ERANGE)
+    (this synchronises the stream)."""
+    _require_device(data, "data", torch.uint8)
+    _require_device(offsets, "offsets", torch.int64)
+    _require_device(sizes, "sizes", torch.int32)
+    n = offsets.numel()
+    if sizes.numel() != n:
+        raise ValueError("offsets and sizes differ in length")
+    if out is None:
+        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+    elif out.numel() < 20 * n:
+        raise ValueError("out too small")
+    if n == 0:
+        return out
+    status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
+    with torch.cuda.device(data.device):
+        check(lib().sf_index_device_blocks(data.data_ptr() if data.numel() else None, data.numel(),
+                                           offsets.data_ptr(), sizes.data_ptr(), n, out.data_ptr(),
+                                           status.data_ptr() if status is not None else None,
+                                           _stream_ptr(data, stream)),
+              "sf_index_device_blocks")
+    if status is not None and int(status.item()) != 0:
+        raise SfError(SF_ERANGE, "sf_index_device_blocks")
+    return out
+
+
+def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], block_size: int,
+                       file_hashes: bool = True, stream: Optional[torch.cuda.Stream] = None):
+    """Many files inside one HBM buffer.
+
+    ``files`` = [(offset, length), ...].  Returns (digests uint8[n,20],
+    first_block int64[n_files+1], file_hashes uint8[n_files,20] or None)."""
+    _require_device(data, "data", torch.uint8)
+    nf = len(files)
+    descs = (FileDesc * max(nf, 1))()
+    total = 0
+    for i, (o, ln) in enumerate(files):
+        descs[i].offset, descs[i].len = int(o), int(ln)
+        total += num_blocks(int(ln), block_size)
+    dig = torch.empty((total, 20), dtype=torch.uint8, device=data.device)
+    fh = torch.empty((nf, 20), dtype=torch.uint8, device=data.device) if file_hashes and nf else None
+    first = np.zeros(nf + 1, np.uint64)
+    nb = ctypes.c_uint64(0)
+    with torch.cuda.device(data.device):
+        check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs, nf,
+                                          block_size, dig.data_ptr() if total else None, total,
+                                          fh.data_ptr() if fh is not None else None,
+                                          first.ctypes.data, ctypes.byref(nb), _stream_ptr(data, stream)),
+              "sf_index_device_batch")
+    return dig, first.astype(np.int64), fh
+
+
+def fill_splitmix(out: torch.Tensor, seed: int, start: int = 0,
+                  stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """Fill a uint8 HBM buffer with bytes [start, start+len) of the
+    splitmix64 stream `seed` (the synthetic input of bench.py / tests)."""
+    _require_device(out, "out", torch.uint8)
+    with torch.cuda.device(out.device):
+        check(lib().sf_fill_splitmix_device(out.data_ptr() if out.numel() else None, out.numel(),
+                                            seed & 0xFFFFFFFFFFFFFFFF, start, _stream_ptr(out, stream)),
+              "sf_fill_splitmix_device")
+    return out
+
+
+def splitmix_tensor(length: int, seed: int, device="cuda", start: int = 0) -> torch.Tensor:
+    t = torch.empty(length, dtype=torch.uint8, device=device)
+    return fill_splitmix(t, seed, start)

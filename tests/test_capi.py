@@ -1,0 +1,116 @@
+"""CPU: the C-ABI library loads, exports what include/syncfast_amd.h declares,
+validates arguments, and its host stage (blocks_hash SHA-1) is exact.
+No GPU compute is called here."""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import syncfast_amd
+from syncfast_amd import _lib, host
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "syncfast_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    L = syncfast_amd.lib()
+    names = header_functions()
+    assert len(names) >= 13
+    assert sorted(_lib.EXPORTED) == names
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_version_and_errors():
+    L = syncfast_amd.lib()
+    assert b"gfx950" in L.sf_version()
+    for code in (_lib.SF_EINVAL, _lib.SF_ENOSPC, _lib.SF_ERANGE, _lib.SF_ENODEV, _lib.SF_EIO, _lib.SF_ENOMEM):
+        assert L.sf_strerror(code).decode() not in ("", "unknown error")
+
+
+def test_struct_layout():
+    assert ctypes.sizeof(_lib.BlockSig) == 32
+    assert _lib.BlockSig.sha1.offset == 12
+    assert ctypes.sizeof(_lib.FileDesc) == 16
+
+
+def test_argument_validation_without_device():
+    L = syncfast_amd.lib()
+    n = ctypes.c_uint64(0)
+    # block size 0 / too large are rejected before any device work
+    assert L.sf_index_device_fixed(None, 100, 0, None, 0, ctypes.byref(n), None) == _lib.SF_EINVAL
+    assert L.sf_index_device_fixed(None, 100, (32 << 20) + 1, None, 0, ctypes.byref(n), None) == _lib.SF_EINVAL
+    # capacity check reports the need
+    assert L.sf_index_device_fixed(None, 10000, 4096, None, 1, ctypes.byref(n), None) == _lib.SF_ENOSPC
+    assert n.value == 3
+    # empty input: zero blocks, nothing launched
+    assert L.sf_index_device_fixed(None, 0, 4096, None, 0, ctypes.byref(n), None) == 0 and n.value == 0
+    assert L.sf_index_device_blocks(None, 0, None, None, 0, None, None, None) == 0
+    assert L.sf_index_device_blocks(None, 5, None, None, 3, None, None, None) == _lib.SF_EINVAL
+    out = np.zeros(4, host.SIG_DTYPE)
+    assert L.sf_index_buffer(None, 0, 4096, out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)), 0,
+                             ctypes.byref(n)) == 0 and n.value == 0
+    assert L.sf_index_file(b"/nonexistent/file", 4096, None, 0, ctypes.byref(n), None) == _lib.SF_EIO
+    assert L.sf_blocks_hash(None, 0, None) == _lib.SF_EINVAL
+
+
+def test_device_count_is_queryable():
+    assert syncfast_amd.device_count() >= 0
+
+
+@pytest.mark.parametrize("length", [0, 1, 55, 56, 63, 64, 65, 119, 120, 1000, 65536 + 7])
+def test_host_sha1_exact(length):
+    data = oracle.splitmix_bytes(length, length + 5).tobytes()
+    want = hashlib.sha1(data).digest()
+    assert host.sha1(data) == want
+    # both host code paths (SHA-NI when present, scalar)
+    L = syncfast_amd.lib()
+    L.sf_host_sha1_impl.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+    for force_scalar in (0, 1):
+        a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+        out = (ctypes.c_uint8 * 20)()
+        L.sf_host_sha1_impl(a.ctypes.data, length, out, force_scalar)
+        assert bytes(out) == want
+
+
+def test_blocks_hash_matches_reference_kat(golden):
+    g = golden["reference_kat"]
+    digs = b"".join(bytes.fromhex(b["sha1"]) for b in g["blocks"])
+    assert host.blocks_hash(digs).hex() == g["blocks_hash"]
+    assert host.blocks_hash(b"").hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
+
+
+def test_blocks_hash_golden(golden):
+    for case in golden["fixed"] + golden["ragged"]:
+        digs = b"".join(bytes.fromhex(h) for h in case["digests"])
+        assert host.blocks_hash(digs).hex() == case["blocks_hash"]
+
+
+def test_blocks_hash_sigs_rows():
+    rows = np.zeros(5, host.SIG_DTYPE)
+    rng = np.random.default_rng(3)
+    rows["sha1"] = rng.integers(0, 256, (5, 20), dtype=np.uint8)
+    out = (ctypes.c_uint8 * 20)()
+    L = syncfast_amd.lib()
+    assert L.sf_blocks_hash_sigs(rows.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)), 5, out) == 0
+    assert bytes(out) == hashlib.sha1(rows["sha1"].tobytes()).digest()
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "syncfast_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                src = open(os.path.join(dirpath, fn), errors="replace").read()
+                assert "import oracle" not in src and "from oracle" not in src, fn
+                assert "sf_oracle" not in src and "sfo_" not in src, fn

@@ -1,0 +1,201 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the oracle, bit for bit.
+
+Sizes are chosen so the oracle finishes in seconds; full-size properties are
+in test_gpu_fullsize.py.  Every case checks all 20 bytes of every digest.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from syncfast_amd import SfError, device, host
+
+pytestmark = pytest.mark.gpu
+
+
+def to_dev(b, dev):
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev) if len(b) else torch.empty(0, dtype=torch.uint8, device=dev)
+
+
+def hexes(d):
+    return [bytes(r).hex() for r in (d.cpu().numpy() if isinstance(d, torch.Tensor) else d)]
+
+
+def test_device_generator_matches_oracle(gpu):
+    for n, seed, start in [(1 << 20, 0x5EED0000, 0), (12345, 7, 3), (4097, 9, 16), (0, 1, 0)]:
+        t = torch.empty(n, dtype=torch.uint8, device=gpu)
+        device.fill_splitmix(t, seed, start)
+        assert np.array_equal(t.cpu().numpy(), oracle.splitmix_bytes(n, seed, start))
+
+
+def test_reference_kat_on_device(gpu, golden):
+    g = golden["reference_kat"]
+    t = to_dev(oracle.kat_input(), gpu)
+    offs = torch.tensor([b["offset"] for b in g["blocks"]], dtype=torch.int64, device=gpu)
+    sizes = torch.tensor([b["size"] for b in g["blocks"]], dtype=torch.int32, device=gpu)
+    d = device.index_device_blocks(t, offs, sizes)
+    assert hexes(d) == [b["sha1"] for b in g["blocks"]]
+    assert host.blocks_hash(d.cpu().numpy()).hex() == g["blocks_hash"]
+
+
+def test_fixed_golden_on_device(gpu, golden):
+    for case in golden["fixed"]:
+        t = torch.empty(case["len"], dtype=torch.uint8, device=gpu)
+        device.fill_splitmix(t, case["seed"])
+        d = device.index_device(t, case["block_size"])
+        assert hexes(d) == case["digests"], (case["len"], case["block_size"])
+        assert host.blocks_hash(d.cpu().numpy()).hex() == case["blocks_hash"]
+
+
+def test_ragged_golden_on_device(gpu, golden):
+    for case in golden["ragged"]:
+        t = torch.empty(case["len"], dtype=torch.uint8, device=gpu)
+        device.fill_splitmix(t, case["seed"])
+        offs = torch.tensor(case["offsets"], dtype=torch.int64, device=gpu)
+        sizes = torch.tensor(case["sizes"], dtype=torch.int32, device=gpu)
+        d = device.index_device_blocks(t, offs, sizes)
+        assert hexes(d) == case["digests"]
+
+
+@pytest.mark.parametrize("bs", [1, 16, 64, 100, 1000, 4095, 4096, 4097, 8192, 65536, 1 << 20])
+def test_fixed_random_lengths(gpu, bs):
+    rng = np.random.default_rng(bs)
+    for _ in range(3):
+        nblk = int(rng.integers(1, 300)) if bs < 65536 else int(rng.integers(1, 40))
+        n = max(0, nblk * bs + int(rng.integers(-bs + 1, bs)))
+        data = oracle.splitmix_bytes(n, int(rng.integers(0, 1 << 62)))
+        d = device.index_device(to_dev(data.tobytes(), gpu), bs)
+        _, _, want = oracle.index_fixed(data, bs)
+        assert np.array_equal(d.cpu().numpy(), want), (bs, n)
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 4, 8, 12, 15])
+def test_misaligned_base_pointer(gpu, shift):
+    # data pointer not 16-B aligned -> the per-lane (non-LDS) path
+    n = 4096 * 70 + 333
+    raw = oracle.splitmix_bytes(n + shift, 5)
+    t = to_dev(raw.tobytes(), gpu)[shift:]
+    assert t.data_ptr() % 16 != 0
+    d = device.index_device(t, 4096)
+    _, _, want = oracle.index_fixed(raw[shift:], 4096)
+    assert np.array_equal(d.cpu().numpy(), want)
+
+
+def test_empty_input(gpu):
+    d = device.index_device(torch.empty(0, dtype=torch.uint8, device=gpu), 4096)
+    assert d.shape == (0, 20)
+
+
+def test_table_unsorted_overlapping_empty_blocks(gpu):
+    rng = np.random.default_rng(11)
+    n = 500_000
+    data = oracle.splitmix_bytes(n, 77)
+    t = to_dev(data.tobytes(), gpu)
+    m = 1000
+    sizes = rng.integers(0, 40_000, m).astype(np.int64)
+    sizes[rng.integers(0, m, 50)] = 0
+    offs = np.array([int(rng.integers(0, n - s + 1)) for s in sizes], np.int64)
+    # a few 16-B aligned runs so some waves take the LDS path
+    offs[:128] = (offs[:128] // 16) * 16
+    d = device.index_device_blocks(t, torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu))
+    want = oracle.index_blocks(data, offs, sizes)
+    assert np.array_equal(d.cpu().numpy(), want)
+
+
+def test_table_aligned_contiguous_blocks(gpu):
+    # every block 16-B aligned and contiguous: all waves on the LDS path, with
+    # ragged per-lane sizes (mixed full tiles + per-lane tails)
+    rng = np.random.default_rng(12)
+    sizes = (rng.integers(1, 600, 777) * 16 + rng.integers(0, 16, 777) * (rng.random(777) < 0.3)).astype(np.int64)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(((sizes + 15) // 16) * 16)[:-1]
+    n = int(offs[-1] + sizes[-1])
+    data = oracle.splitmix_bytes(n, 78)
+    t = to_dev(data.tobytes(), gpu)
+    d = device.index_device_blocks(t, torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu))
+    assert np.array_equal(d.cpu().numpy(), oracle.index_blocks(data, offs, sizes))
+
+
+def test_table_out_of_range_reports_erange(gpu):
+    t = to_dev(b"x" * 1000, gpu)
+    offs = torch.tensor([0, 990], dtype=torch.int64, device=gpu)
+    sizes = torch.tensor([10, 11], dtype=torch.int32, device=gpu)
+    with pytest.raises(SfError) as e:
+        device.index_device_blocks(t, offs, sizes)
+    assert e.value.code == -34
+
+
+def test_batch_contiguous_files(gpu):
+    nfiles, flen, bs = 37, 8 * 4096, 4096
+    data = oracle.splitmix_bytes(nfiles * flen, 90)
+    t = to_dev(data.tobytes(), gpu)
+    files = [(i * flen, flen) for i in range(nfiles)]
+    dig, first, fh = device.index_device_batch(t, files, bs)
+    _, _, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(dig.cpu().numpy(), want)
+    assert list(first) == [i * 8 for i in range(nfiles + 1)]
+    fhn = fh.cpu().numpy()
+    for i in range(nfiles):
+        assert bytes(fhn[i]) == oracle.blocks_hash(want[8 * i:8 * i + 8])
+
+
+def test_batch_ragged_files(gpu):
+    rng = np.random.default_rng(91)
+    bs = 4096
+    lens = [int(x) for x in rng.integers(0, 60_000, 50)]
+    lens[3] = 0
+    lens[7] = 4096 * 3
+    offs, o = [], 0
+    for ln in lens:
+        offs.append(o)
+        o += ln + int(rng.integers(0, 40))  # gaps, unaligned file starts
+    data = oracle.splitmix_bytes(o, 92)
+    t = to_dev(data.tobytes(), gpu)
+    dig, first, fh = device.index_device_batch(t, list(zip(offs, lens)), bs)
+    dign, fhn = dig.cpu().numpy(), fh.cpu().numpy()
+    for i, (fo, ln) in enumerate(zip(offs, lens)):
+        _, _, want = oracle.index_fixed(data[fo:fo + ln], bs)
+        got = dign[first[i]:first[i + 1]]
+        assert np.array_equal(got, want), i
+        assert bytes(fhn[i]) == oracle.blocks_hash(want), i
+
+
+def test_index_buffer_end_to_end(gpu):
+    n = 3 * (256 << 20) // 2 + 12345  # > one pipeline stage
+    data = oracle.splitmix_bytes(n, 93)
+    rows = host.index_buffer(data, 4096)
+    want = oracle.index_fixed_mt(data, 4096, 8)
+    assert np.array_equal(rows["sha1"], want)
+    assert rows["offset"][1] == 4096 and int(rows["size"].sum()) == n
+
+
+def test_index_file_end_to_end(gpu):
+    data = oracle.splitmix_bytes(5 * 1000 * 1000 + 7, 94)
+    with tempfile.NamedTemporaryFile(delete=False) as f:
+        f.write(data.tobytes())
+        path = f.name
+    try:
+        rows, bh = host.index_file(path, 65536)
+    finally:
+        os.unlink(path)
+    _, _, want = oracle.index_fixed(data, 65536)
+    assert np.array_equal(rows["sha1"], want)
+    assert bh == oracle.blocks_hash(want)
+
+
+def test_block_digest_independent_of_neighbours(gpu):
+    # the same block bytes at different positions / in different waves give
+    # the same digest (no cross-lane leakage through the LDS tile)
+    bs = 4096
+    blk = oracle.splitmix_bytes(bs, 1234)
+    noise = oracle.splitmix_bytes(200 * bs, 4321)
+    buf = noise.copy()
+    for i in (0, 63, 64, 65, 127, 199):
+        buf[i * bs:(i + 1) * bs] = blk
+    d = device.index_device(to_dev(buf.tobytes(), gpu), bs).cpu().numpy()
+    ref = oracle.sha1(blk)
+    for i in (0, 63, 64, 65, 127, 199):
+        assert bytes(d[i]) == ref
