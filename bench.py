@@ -116,6 +116,7 @@ def main():
     if cfg["files"] > 1:
         flen = shard // cfg["files"]
         files = [(i * flen, flen) for i in range(cfg["files"])]
+    fhash = torch.empty((len(files), 20), dtype=torch.uint8, device=dev) if files else None
     gathered = None
     if distributed and not a.no_gather and rank == 0:
         gathered = [torch.empty_like(dig) for _ in range(world)]
@@ -130,7 +131,8 @@ def main():
         if files is None:
             device.index_device(data, bs, out=dig, stream=stream)
         else:
-            device.index_device_batch(data, files, bs, file_hashes=True, stream=stream)
+            device.index_device_batch(data, files, bs, file_hashes=True, out=dig, hashes_out=fhash,
+                                      stream=stream)
         if i is not None:
             ev[i][1].record(stream)
         if distributed and not a.no_gather:

@@ -102,7 +102,8 @@ def index_device_blocks(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.
 
 
 def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], block_size: int,
-                       file_hashes: bool = True, stream: Optional[torch.cuda.Stream] = None):
+                       file_hashes: bool = True, out: Optional[torch.Tensor] = None,
+                       hashes_out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None):
     """Many files inside one HBM buffer.
 
     ``files`` = [(offset, length), ...].  Returns (digests uint8[n,20],
@@ -114,13 +115,21 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
     for i, (o, ln) in enumerate(files):
         descs[i].offset, descs[i].len = int(o), int(ln)
         total += num_blocks(int(ln), block_size)
-    dig = torch.empty((total, 20), dtype=torch.uint8, device=data.device)
-    fh = torch.empty((nf, 20), dtype=torch.uint8, device=data.device) if file_hashes and nf else None
+    if out is None:
+        out = torch.empty((total, 20), dtype=torch.uint8, device=data.device)
+    elif out.numel() < 20 * total:
+        raise ValueError("out too small")
+    dig = out
+    fh = None
+    if file_hashes and nf:
+        fh = hashes_out if hashes_out is not None else torch.empty((nf, 20), dtype=torch.uint8, device=data.device)
+        if fh.numel() < 20 * nf:
+            raise ValueError("hashes_out too small")
     first = np.zeros(nf + 1, np.uint64)
     nb = ctypes.c_uint64(0)
     with torch.cuda.device(data.device):
         check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs, nf,
-                                          block_size, dig.data_ptr() if total else None, total,
+                                          block_size, dig.data_ptr() if total else None, dig.numel() // 20,
                                           fh.data_ptr() if fh is not None else None,
                                           first.ctypes.data, ctypes.byref(nb), _stream_ptr(data, stream)),
               "sf_index_device_batch")
