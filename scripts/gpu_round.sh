@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Stops at the first step that crashes / times out (exit >= 2 from pytest
+# means an internal error; 124/137/134/139 mean timeout/kill/abort/segv).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS="${STEPS:-10}"
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -5 "gpurun_out/$name.log"
+  return $rc
+}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+rc=$?; if [ $rc -ge 2 ]; then exit $rc; fi
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+run bench 600 python bench.py --steps "$STEPS" --warmup 2 --cpu-seconds 8 || exit $?
+if [ -n "$PROFILE" ]; then
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+fi
+exit $rc
