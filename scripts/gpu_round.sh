@@ -14,11 +14,18 @@ run() {  # name timeout cmd...
   echo "== $name rc=$rc"; tail -5 "gpurun_out/$name.log"
   return $rc
 }
+if [ -n "$PROBE" ]; then
+  run valu_probe 300 ./scripts/valu_probe || exit $?
+fi
 run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
 rc=$?; if [ $rc -ge 2 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 2 --cpu-seconds 8 || exit $?
 if [ -n "$PROFILE" ]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+  B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B || exit $?
+  run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o pmc -- $B || exit $?
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o pmc -- $B || exit $?
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o pmc -- $B || exit $?
 fi
 exit $rc

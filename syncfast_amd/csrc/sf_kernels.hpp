@@ -36,6 +36,13 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // raw buffer, gfx9 family
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // ---------------------------------------------------------- wave helpers
+// A value identical in every lane, moved to SGPRs so that everything derived
+// from it (buffer resources, loop bounds) stays scalar.
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
@@ -52,7 +59,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     uint64_t o = __shfl_xor((unsigned long long)v, m, 64);
     v = o < v ? o : v;
   }
-  return v;  // identical in every lane
+  return uniform_u64(v);
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
@@ -60,7 +67,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     uint64_t o = __shfl_xor((unsigned long long)v, m, 64);
     v = o > v ? o : v;
   }
-  return v;
+  return uniform_u64(v);
 }
 
 __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
@@ -115,11 +122,14 @@ struct WaveGeo {
 template <int TILE>
 __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t span, uint32_t step,
                                            const uint32_t (&voff)[TILE / 16], uint4* wave_tile) {
+  // All operands are wave-uniform; readfirstlane keeps the resource in SGPRs
+  // (a VGPR resource makes hipcc wrap every DMA in a waterfall loop).
   const uint64_t toff = (uint64_t)step * TILE;
   const uint64_t left = span > toff ? span - toff : 0;
-  const uint32_t nrec = left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left;
+  const uint32_t nrec = __builtin_amdgcn_readfirstlane(left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left);
+  const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
   __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(span_ptr + toff), (short)0, (int)nrec, (int)kRsrcWord3);
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
 #pragma unroll
   for (int j = 0; j < TILE / 16; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, 0);
@@ -215,9 +225,9 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
                   uint8_t* __restrict__ digests) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
-  if (first >= nblocks) return;  // wave-uniform
+  if (first >= nblocks) return;
   const uint64_t blk = first + lane;
   const bool valid = blk < nblocks;
   const uint64_t off = valid ? blk * bs : first * bs;
@@ -251,7 +261,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
                   int* __restrict__ status) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
   if (first >= nblocks) return;
   const uint64_t blk = first + lane;
@@ -276,7 +286,8 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
   geo.max_nch = wave_max_u32(valid ? n_chunks(size) : 0u);
   const bool aligned = !valid || ((off & 15u) == 0);
-  geo.lds_ok = __all(aligned) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
+  geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
+               ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 
   Sha1 st;

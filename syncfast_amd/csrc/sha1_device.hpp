@@ -7,8 +7,7 @@
 // Cost model (CDNA4): one 64-byte compression = 80 rounds x 5 VALU
 // (v_alignbit rotl5, v_bitop3 f, 2 x v_add3, v_alignbit rotl30) + 64 x 3
 // schedule ops (v_bitop3 xor3, v_xor, v_alignbit rotl1) + 16 v_perm byte swaps
-// + 5 feed-forward adds ~= 613 VALU per 64 B.  hipcc forms all of these from
-// the plain C++ below (checked in the .s).
+// + 5 feed-forward adds ~= 613 VALU per 64 B (checked in the .s: make isa).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,6 +19,19 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Three-input boolean functions as ONE v_bitop3_b32 (gfx950).  The immediate
+// is the truth table over (S0=0xF0, S1=0xCC, S2=0xAA).  hipcc does not form
+// v_bitop3 from a^b^c on its own (it emits two v_xor_b32), so spell it out.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t b, uint32_t c, uint32_t d) {  // (b & c) | (~b & d)
+  return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t b, uint32_t c, uint32_t d) {  // (b&c) | (b&d) | (c&d)
+  return __builtin_amdgcn_bitop3_b32(b, c, d, 0xE8);
+}
 
 struct Sha1 {
   uint32_t h0, h1, h2, h3, h4;
@@ -36,14 +48,14 @@ struct Sha1 {
       if (t < 16) {
         wt = w[t];
       } else {
-        wt = rotl(w[(t + 13) & 15] ^ w[(t + 8) & 15] ^ w[(t + 2) & 15] ^ w[t & 15], 1);
+        wt = rotl(xor3(w[(t + 13) & 15], w[(t + 8) & 15], w[(t + 2) & 15]) ^ w[t & 15], 1);
         w[t & 15] = wt;
       }
       uint32_t f, k;
-      if (t < 20) { f = d ^ (b & (c ^ d)); k = 0x5A827999u; }
-      else if (t < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
-      else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8F1BBCDCu; }
-      else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+      if (t < 20) { f = ch(b, c, d); k = 0x5A827999u; }
+      else if (t < 40) { f = xor3(b, c, d); k = 0x6ED9EBA1u; }
+      else if (t < 60) { f = maj(b, c, d); k = 0x8F1BBCDCu; }
+      else { f = xor3(b, c, d); k = 0xCA62C1D6u; }
       const uint32_t tmp = rotl(a, 5) + f + e + k + wt;
       e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
     }
