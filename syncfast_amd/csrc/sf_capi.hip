@@ -23,6 +23,13 @@ namespace {
 
 constexpr int kTile = 128;  // bytes of each block staged per LDS step
 
+// Tuning knob for experiments (interleaved A/B in one process): SF_TILE=64
+// selects the 64-B staging variant.  Read on every call.
+inline int tile_choice() {
+  const char* e = getenv("SF_TILE");
+  return (e && atoi(e) == 64) ? 64 : kTile;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int hip_err(hipError_t e) {
@@ -44,12 +51,38 @@ inline unsigned grid_for_blocks(uint64_t nblocks) {
   return (unsigned)ceil_div(waves, sf::kWavesPerWG);
 }
 
+// K_t + W_t for the padding-only chunk of a `bytes`-long message (bytes a
+// multiple of 64): W = {0x80000000, 0 x 13, bit length hi, lo}.
+sf::PadSchedule pad_schedule(uint32_t bytes) {
+  sf::PadSchedule p{};
+  if (bytes == 0 || (bytes & 63u)) return p;
+  uint32_t w[80] = {0};
+  w[0] = 0x80000000u;
+  w[14] = bytes >> 29;
+  w[15] = bytes << 3;
+  for (int t = 16; t < 80; t++) {
+    const uint32_t x = w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16];
+    w[t] = (x << 1) | (x >> 31);
+  }
+  for (int t = 0; t < 80; t++) {
+    const uint32_t k = t < 20 ? 0x5A827999u : t < 40 ? 0x6ED9EBA1u : t < 60 ? 0x8F1BBCDCu : 0xCA62C1D6u;
+    p.kw[t] = k + w[t];
+  }
+  p.bytes = bytes;
+  return p;
+}
+
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
                  hipStream_t stream) {
   if (nblocks == 0) return SF_OK;
   const unsigned grid = grid_for_blocks(nblocks);
-  hipLaunchKernelGGL(sf::sha1_fixed_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
-                     static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests));
+  const sf::PadSchedule pad = pad_schedule(bs);
+  if (tile_choice() == 64)
+    hipLaunchKernelGGL(sf::sha1_fixed_kernel<64>, dim3(grid), dim3(sf::kThreads), 0, stream,
+                       static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests), pad);
+  else
+    hipLaunchKernelGGL(sf::sha1_fixed_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
+                       static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests), pad);
   return hip_err(hipGetLastError());
 }
 

@@ -107,11 +107,19 @@ __device__ __forceinline__ void build_tail_chunk(uint32_t (&w)[16], const uint8_
   }
 }
 
+// K_t + W_t of the padding-only chunk ending a block of `bytes` bytes
+// (bytes % 64 == 0), filled by the host (sf_capi.hip) and passed by value.
+struct PadSchedule {
+  uint32_t bytes;  // 0 = not available
+  uint32_t kw[80];
+};
+
 // Per-wave geometry of the blocks handled by this wave.
 struct WaveGeo {
   uint64_t base;      // byte offset of the wave's span in `data`
   uint64_t span;      // bytes in [base, end of last block)
   uint32_t min_size;  // min block size over valid lanes
+  uint32_t max_size;  // max block size over valid lanes
   uint32_t max_nch;   // max compressions over valid lanes
   bool lds_ok;        // 16-B aligned pieces and span < 4 GiB
 };
@@ -141,7 +149,7 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
 template <int TILE>
 __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
                                           uint32_t rel, bool valid, const WaveGeo& geo,
-                                          uint4* __restrict__ wave_tile, Sha1& st) {
+                                          uint4* __restrict__ wave_tile, Sha1& st, const PadSchedule* pad) {
   constexpr int PIECES = TILE / 16;           // 16-B pieces per block per step
   constexpr int CH = TILE / 64;               // compressions per step
   constexpr int GSHIFT = PIECES == 4 ? 2 : (PIECES == 8 ? 1 : 0);
@@ -205,6 +213,12 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     }
     c_done = nfull;
   }
+  // Every block of the wave has the same 64-B multiple size and all its data
+  // chunks are done: the last chunk is the same padding for every lane.
+  if (pad && pad->bytes == geo.min_size && geo.min_size == geo.max_size && c_done == nfull) {
+    st.compress_uniform(pad->kw);
+    return;
+  }
   // Remaining data chunks and the padding chunk(s), per lane.
   const uint32_t nch = n_chunks(size);
   for (uint32_t c = c_done; c < geo.max_nch; ++c) {
@@ -222,7 +236,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 template <int TILE>
 __global__ void __launch_bounds__(kThreads)
 sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                  uint8_t* __restrict__ digests) {
+                  uint8_t* __restrict__ digests, const PadSchedule pad) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
@@ -239,13 +253,14 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   geo.span = len - geo.base < (last - first + 1) * (uint64_t)bs ? len - geo.base : (last - first + 1) * (uint64_t)bs;
   const uint32_t last_size = (uint32_t)(len - last * bs < bs ? len - last * bs : bs);
   geo.min_size = last_size < bs ? last_size : bs;
+  geo.max_size = bs;
   geo.max_nch = n_chunks(bs);
   geo.lds_ok = ((bs & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
                (64ull * bs < 0xF0000000ull);
   const uint32_t rel = (uint32_t)((uint64_t)lane * bs);
 
   Sha1 st;
-  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st);
+  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, &pad);
   if (valid) st.store(digests + blk * 20);
 }
 
@@ -284,6 +299,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   geo.base = lo;
   geo.span = hi - lo;
   geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
+  geo.max_size = wave_max_u32(valid ? size : 0u);
   geo.max_nch = wave_max_u32(valid ? n_chunks(size) : 0u);
   const bool aligned = !valid || ((off & 15u) == 0);
   geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
@@ -291,7 +307,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 
   Sha1 st;
-  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st);
+  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, nullptr);
   if (valid) {
     if (bad) {
       uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);

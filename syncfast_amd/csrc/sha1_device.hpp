@@ -61,6 +61,25 @@ struct Sha1 {
     }
     h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
   }
+  // Compression of a chunk whose message words are the same for every lane
+  // (the padding-only chunk ending a message of a 64-B multiple length).
+  // kw[t] = K_t + W_t is precomputed on the host and arrives as kernel
+  // arguments (SGPRs), so each round costs 4 VALU (rotl5, f, add3, add) and
+  // there is no per-lane message schedule.
+  __device__ __forceinline__ void compress_uniform(const uint32_t (&kw)[80]) {
+    uint32_t a = h0, b = h1, c = h2, d = h3, e = h4;
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+      uint32_t f;
+      if (t < 20) f = ch(b, c, d);
+      else if (t < 40) f = xor3(b, c, d);
+      else if (t < 60) f = maj(b, c, d);
+      else f = xor3(b, c, d);
+      const uint32_t tmp = rotl(a, 5) + f + e + kw[t];
+      e = d; d = c; c = rotl(b, 30); b = a; a = tmp;
+    }
+    h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
+  }
   // Digest bytes in sha1.digest().bytes() order (big-endian), as 5 words
   // ready for a little-endian store.
   __device__ __forceinline__ void store(uint8_t* out20) const {
