@@ -37,6 +37,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from syncfast_amd import device, host  # noqa: E402
+from syncfast_amd.shard import gather_digests, shard_range  # noqa: E402
 
 GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
@@ -62,6 +63,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
 
@@ -95,58 +97,82 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % ndev)  # % only matters for single-GPU rehearsals
+    torch.cuda.set_device(dev)
     distributed = world > 1
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     cfg = CONFIGS[a.config]
     bs = cfg["block"]
-    shard = int(a.shard_gib * GiB) if a.shard_gib else cfg["bytes"]
-    shard -= shard % bs
+    per_rank = int(a.shard_gib * GiB) if a.shard_gib else cfg["bytes"]
+    per_rank -= per_rank % bs
+    total = per_rank * world  # one logical file, weak scaling: per-GPU bytes fixed
+    start, shard = shard_range(total, bs, world, rank)
     nblk = shard // bs
 
-    # Synthetic input, generated in HBM: rank r holds bytes
-    # [r*shard, (r+1)*shard) of one logical file (seed SEED).
+    # Synthetic input, generated in HBM: rank r holds bytes [start,
+    # start+shard) of one logical file (seed SEED).
     data = torch.empty(shard, dtype=torch.uint8, device=dev)
-    device.fill_splitmix(data, SEED, rank * shard)
-    dig = torch.empty((nblk, 20), dtype=torch.uint8, device=dev)
+    device.fill_splitmix(data, SEED, start)
+    # Two digest tables: step i writes table i%2 while the gather of step
+    # i-1's table is still in flight (RCCL runs on its own stream).
+    digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=dev) for _ in range(2)]
     files = None
     if cfg["files"] > 1:
         flen = shard // cfg["files"]
         files = [(i * flen, flen) for i in range(cfg["files"])]
     fhash = torch.empty((len(files), 20), dtype=torch.uint8, device=dev) if files else None
-    gathered = None
-    if distributed and not a.no_gather and rank == 0:
-        gathered = [torch.empty_like(dig) for _ in range(world)]
+    gather = distributed and not a.no_gather
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    pending = [None, None]
+    last_table = [None]
 
-    def step(i=None):
-        if i is not None:
+    def step(i, timed):
+        b = i % 2
+        if pending[b] is not None:  # the gather that reads digs[b] must be done
+            work, finish = pending[b]
+            work.wait()
+            last_table[0] = finish()
+            pending[b] = None
+        if timed:
             ev[i][0].record(stream)
         if files is None:
-            device.index_device(data, bs, out=dig, stream=stream)
+            device.index_device(data, bs, out=digs[b], stream=stream)
         else:
-            device.index_device_batch(data, files, bs, file_hashes=True, out=dig, hashes_out=fhash,
+            device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
                                       stream=stream)
-        if i is not None:
+        if timed:
             ev[i][1].record(stream)
-        if distributed and not a.no_gather:
-            dist.gather(dig, gathered if rank == 0 else None, dst=0)
+        if gather:
+            pending[b] = gather_digests(digs[b], total, bs, async_op=True)
 
-    for _ in range(a.warmup):
-        step()
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                work, finish = pending[b]
+                work.wait()
+                last_table[0] = finish()
+                pending[b] = None
+
+    for i in range(a.warmup):
+        step(i, False)
+    drain()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step(i)
+        step(i, True)
+    drain()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -155,10 +181,14 @@ def main():
     kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
     kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
     if distributed:
+        if a.dist_backend == "gloo":
+            elapsed, kt = elapsed.cpu(), kt.cpu()
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
     t = float(elapsed.item())
     kern_ms = float(kt.item())
+    dig = digs[(a.steps - 1) % 2]
+    gathered = last_table[0]
 
     # Self-check (product host SHA-1): first and last block of this shard.
     d = dig.cpu().numpy()
@@ -171,16 +201,19 @@ def main():
             dist.destroy_process_group()
         return
 
+    if gathered is not None:  # rank 0 owns the whole file's table, rank order
+        assert gathered.shape[0] == total // bs and torch.equal(gathered[:nblk].to(dig.device), dig)
+
     # Host stage of the single-file path: blocks_hash over all digests
     # (sequential SHA-1, reported separately, not in `value`).
     bh_ms = None
     if files is None:
-        full = torch.cat(gathered).cpu().numpy() if gathered else d
+        full = gathered.cpu().numpy() if gathered is not None else d
         tb = time.perf_counter()
         host.blocks_hash(full)
         bh_ms = (time.perf_counter() - tb) * 1e3
 
-    total_bytes = shard * world
+    total_bytes = total
     gibs = total_bytes / GiB / (t / a.steps)
     alg_bytes = nblk * (bs + 20)  # read every byte once + write 20 B/block
     if files is not None:  # + per-file blocks_hash kernel: re-read the digests, write 20 B/file
@@ -214,7 +247,8 @@ def main():
         "data": "synthetic (splitmix64 bytes generated in HBM, seed 0x5EED0000)",
         "config": {"workload": cfg["workload"], "bytes_per_gpu": shard, "block_size": bs,
                    "total_bytes": total_bytes, "files": cfg["files"], "blocks": nblk * world,
-                   "parallelism": f"shard{world}" + ("+rccl_gather" if distributed and not a.no_gather else "")},
+                   "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else a.dist_backend}"
+                                                     "_gather(pipelined)" if gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "sha1_fixed_kernel<128>", "kernel_ms": round(kern_ms, 4),

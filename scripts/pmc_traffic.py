@@ -1,0 +1,42 @@
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into profiles/traffic.json.
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
+coalesced streaming read (16 B/lane loads and buffer_load ... lds alike), so it
+is doubled; WRITE_SIZE is exact for streaming stores.  Averages over every
+launch of the SHA-1 kernel in the pass.
+
+usage: python scripts/pmc_traffic.py FETCH_CSV WRITE_CSV CONFIG_KEY SHARD_BYTES [OUT]
+"""
+import csv
+import json
+import os
+import sys
+
+
+def avg(path, counter, match="sha1_fixed_kernel"):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if match in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    fetch_csv, write_csv, key, shard = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json")
+    f, nf = avg(fetch_csv, "FETCH_SIZE")
+    w, nw = avg(write_csv, "WRITE_SIZE")
+    read_b = f * 1024 * 2
+    write_b = w * 1024
+    data = {}
+    if os.path.exists(out):
+        data = json.load(open(out))
+    data[key] = {"shard_bytes": shard, "hbm_bytes_per_launch": int(read_b + write_b),
+                 "read_bytes": int(read_b), "write_bytes": int(write_b), "launches": [nf, nw],
+                 "raw_kib": {"FETCH_SIZE": f, "WRITE_SIZE": w},
+                 "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"}
+    json.dump(data, open(out, "w"), indent=1)
+    print(json.dumps(data[key]))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""Multi-GPU sharding of one logical file + RCCL gather of the signature table.
+
+The reference indexes one file on one thread (src/index.rs:610-659).  Blocks
+are independent, so a file splits into contiguous, block-aligned shards, one
+per rank (one process per GPU, torch.distributed over RCCL/xGMI); each rank
+hashes its shard with no communication.  The only exchange is the one the
+single-file ``blocks_hash`` needs (src/index.rs:661-682 hashes ALL of a
+file's digests in order): every shard's 20-byte digest table is gathered to
+rank 0, which then owns the full (offset, size, SHA-1) table.
+
+Everything here is backend-agnostic torch.distributed, so the same code runs
+over RCCL on MI355X and over gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total_len: int, block_size: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, block-aligned byte range [start, start+len) of `rank`.
+
+    Blocks are dealt as evenly as possible (the first `nblocks % world` ranks
+    get one extra); a rank may get an empty range.  Block i of the file is
+    block (i - first_block) of the shard that holds it, so the concatenation
+    of the shards' digest tables in rank order is the file's table."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    nblocks = (total_len + block_size - 1) // block_size if total_len else 0
+    per, extra = divmod(nblocks, world)
+    first = rank * per + min(rank, extra)
+    count = per + (1 if rank < extra else 0)
+    start = min(total_len, first * block_size)
+    end = min(total_len, (first + count) * block_size)
+    return start, max(0, end - start)
+
+
+def shard_blocks(total_len: int, block_size: int, world: int) -> List[int]:
+    """Number of blocks of every rank's shard."""
+    out = []
+    for r in range(world):
+        _, ln = shard_range(total_len, block_size, world, r)
+        out.append((ln + block_size - 1) // block_size if ln else 0)
+    return out
+
+
+def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
+                   group: Optional[dist.ProcessGroup] = None, dst: int = 0,
+                   async_op: bool = False):
+    """Gather every rank's uint8[n_r, 20] digest table to `dst`.
+
+    Ranks may hold different block counts (uneven last shard): tables are
+    padded to the largest shard for the collective and trimmed on `dst`.
+    Returns the full uint8[n, 20] table on `dst` (None elsewhere); with
+    async_op, returns (work, finish) where finish() -> table after
+    work.wait()."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    counts = shard_blocks(total_len, block_size, world)
+    if local.shape[0] != counts[rank]:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} digests, shard has {counts[rank]}")
+    m = max(counts) if counts else 0
+    if dist.get_backend(group) == "gloo" and local.device.type != "cpu":
+        local = local.cpu()  # gloo gathers host tensors (rehearsal / CPU tests only)
+    if local.shape[0] != m:
+        padded = torch.zeros((m, 20), dtype=torch.uint8, device=local.device)
+        padded[:local.shape[0]] = local
+    else:
+        padded = local
+    bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+    work = dist.gather(padded, bufs, dst=dst, group=group, async_op=async_op)
+
+    def finish():
+        if rank != dst:
+            return None
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+    if async_op:
+        return work, finish
+    return finish()
