@@ -1,0 +1,382 @@
+"""Index -- syncfast's library index API with the signatures computed on MI355X.
+
+Mirrors ``pub struct Index`` (/root/reference/src/index.rs:43-736): the same
+SQLite schema (src/index.rs:12-38), the same methods and row semantics, so
+callers written against the reference (the CLI ``index`` command,
+src/main.rs:111-124, and the sync endpoints, src/sync/fs.rs:53-58, 239-248,
+463) see identical data.  What changes is the hot path inside
+``index_file`` (src/index.rs:610-659): instead of a per-byte CPU loop and one
+SQL INSERT per block, the file's bytes go through the C-ABI to the gfx950
+SHA-1 kernel and the rows are inserted in one batch.
+
+Chunking.  The reference cuts blocks with the third-party cdchunking 0.2.1
+ZPAQ chunker (src/index.rs:622-625), whose recurrence is not available here
+(CDC parity unpinned).  ``Index`` therefore takes a chunker:
+``FixedChunker(block_size)`` (the BASELINE configs) or ``BoundaryChunker``
+(any boundary function, e.g. the reference KAT boundaries); the per-block
+SHA-1, the rows, ``blocks_hash`` and every query are bit-identical to the
+reference for the same boundaries.
+
+Quirks kept on purpose: ``index_file`` leaves ``files.size`` NULL (the
+reference never sets it there, so ``list_files`` reports 0, src/index.rs:
+376-377); ``compute_blocks_hash`` hashes the digests in the order SQLite
+returns them for ``WHERE file_id = ?`` with no ORDER BY (src/index.rs:663-
+669), which is insertion (= offset) order.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import logging
+import os
+import sqlite3
+from pathlib import Path, PurePath
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import host
+from .digest import HashDigest
+
+log = logging.getLogger("syncfast_amd.index")
+
+SCHEMA = """
+    CREATE TABLE files(
+        file_id INTEGER NOT NULL PRIMARY KEY,
+        name VARCHAR(512) NOT NULL,
+        modified DATETIME NOT NULL,
+        size INTEGER NULL,
+        blocks_hash VARCHAR(40) NULL,
+        temporary BOOLEAN NOT NULL
+    );
+    CREATE INDEX idx_files_name ON files(name);
+
+    CREATE TABLE blocks(
+        file_id INTEGER NOT NULL,
+        hash VARCHAR(40) NOT NULL,
+        offset INTEGER NOT NULL,
+        size INTEGER NOT NULL,
+        present BOOLEAN NOT NULL,
+        PRIMARY KEY(file_id, offset)
+    );
+    CREATE INDEX idx_blocks_file_id ON blocks(file_id);
+    CREATE INDEX idx_blocks_hash ON blocks(hash);
+    CREATE INDEX idx_blocks_offset ON blocks(file_id, offset);
+    CREATE INDEX idx_blocks_present ON blocks(file_id, present);
+
+    PRAGMA application_id=0x51367457;
+    PRAGMA user_version=0x00000000;
+"""
+
+INDEX_FILE_NAME = ".syncfast.idx"  # src/index.rs:699, src/main.rs:117
+TEMP_PREFIX = ".syncfast_tmp_"     # src/lib.rs:152
+
+
+class SyncfastError(Exception):
+    """Error (src/lib.rs:24-31): Io / Sqlite / BadFilenameEncoding."""
+
+
+def temp_name(name) -> PurePath:
+    """src/lib.rs:147-158: dir/file -> dir/.syncfast_tmp_file."""
+    p = PurePath(name)
+    if not p.name:
+        raise SyncfastError("Invalid path")
+    return p.with_name(TEMP_PREFIX + p.name)
+
+
+def untemp_name(name) -> PurePath:
+    """src/lib.rs:160-174."""
+    p = PurePath(name)
+    if not p.name.startswith(TEMP_PREFIX):
+        raise SyncfastError("Not a temporary path")
+    return p.with_name(p.name[len(TEMP_PREFIX):])
+
+
+def _name_str(name) -> str:
+    s = str(PurePath(name)) if str(name) != "" else ""
+    try:
+        s.encode("utf-8")
+    except UnicodeEncodeError:
+        raise SyncfastError("BadFilenameEncoding") from None
+    return s
+
+
+def _ts(dt: _dt.datetime) -> str:
+    """DateTime<Utc> as text (RFC 3339, UTC)."""
+    return dt.astimezone(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%f+00:00")
+
+
+def _mtime(path) -> _dt.datetime:
+    st = os.stat(path)
+    return _dt.datetime.fromtimestamp(st.st_mtime_ns / 1e9, tz=_dt.timezone.utc)
+
+
+# ----------------------------------------------------------------- chunkers
+
+class FixedChunker:
+    """Blocks of `block_size` bytes (last one shorter); no empty blocks."""
+
+    def __init__(self, block_size: int = 4096):
+        if not 0 < block_size <= (32 << 20):
+            raise ValueError("block_size must be in (0, 32 MiB]")
+        self.block_size = block_size
+
+
+class BoundaryChunker:
+    """Blocks from a boundary function: fn(data: bytes) -> list of block
+    sizes (positive, summing to len(data)).  The signatures are still
+    computed by the GPU kernel (explicit-block-list entry point)."""
+
+    def __init__(self, fn: Callable[[bytes], Sequence[int]]):
+        self.fn = fn
+
+
+Chunker = object  # FixedChunker | BoundaryChunker
+
+
+def signatures_of_bytes(data, chunker) -> List[Tuple[int, int, bytes]]:
+    """(offset, size, digest) rows of one file's bytes, computed on the GPU."""
+    if isinstance(chunker, FixedChunker):
+        return host.rows_to_tuples(host.index_buffer(data, chunker.block_size))
+    if isinstance(chunker, BoundaryChunker):
+        import torch
+        from . import device
+        raw = bytes(data)
+        sizes = [int(s) for s in chunker.fn(raw)]
+        if any(s <= 0 for s in sizes) or sum(sizes) != len(raw):
+            raise ValueError("boundary function must return positive sizes covering the data")
+        offs = np.zeros(len(sizes), np.int64)
+        if sizes:
+            offs[1:] = np.cumsum(sizes)[:-1]
+        if not sizes:
+            return []
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        dig = device.index_device_blocks(t, torch.from_numpy(offs).to(dev),
+                                         torch.tensor(sizes, dtype=torch.int32, device=dev)).cpu().numpy()
+        return [(int(o), int(s), bytes(d)) for o, s, d in zip(offs, sizes, dig)]
+    raise TypeError("unknown chunker")
+
+
+# -------------------------------------------------------------------- Index
+
+class Index:
+    """Index of files and blocks (src/index.rs:43-47)."""
+
+    def __init__(self, db: sqlite3.Connection, chunker=None):
+        self.db = db
+        self.in_transaction = False
+        self.chunker = chunker if chunker is not None else FixedChunker(4096)
+
+    # -- open / transactions (src/index.rs:51-74, 729-735)
+    @classmethod
+    def open(cls, filename, chunker=None) -> "Index":
+        exists = os.path.exists(filename)
+        db = sqlite3.connect(str(filename), isolation_level=None)
+        if not exists:
+            log.warning("Database doesn't exist, creating tables...")
+            db.executescript(SCHEMA)
+        return cls(db, chunker)
+
+    @classmethod
+    def open_in_memory(cls, chunker=None) -> "Index":
+        db = sqlite3.connect(":memory:", isolation_level=None)
+        db.executescript(SCHEMA)
+        return cls(db, chunker)
+
+    def begin(self) -> None:
+        if not self.in_transaction:
+            self.db.execute("BEGIN IMMEDIATE;")
+            self.in_transaction = True
+
+    def commit(self) -> None:
+        if self.in_transaction:
+            self.db.execute("COMMIT")
+            self.in_transaction = False
+
+    # -- queries (src/index.rs:77-384, 453-607)
+    def get_block(self, hash: HashDigest) -> Optional[Tuple[PurePath, int, int]]:
+        row = self.db.execute(
+            "SELECT files.name, blocks.offset, blocks.size FROM blocks "
+            "INNER JOIN files ON blocks.file_id = files.file_id "
+            "WHERE blocks.hash = ? AND blocks.present = 1;", (hash.to_sql(),)).fetchone()
+        return (PurePath(row[0]), int(row[1]), int(row[2])) if row else None
+
+    def get_file(self, name) -> Optional[Tuple[int, str, Optional[HashDigest]]]:
+        row = self.db.execute(
+            "SELECT file_id, modified, blocks_hash FROM files WHERE name = ? AND temporary = 0;",
+            (_name_str(name),)).fetchone()
+        if not row:
+            return None
+        return int(row[0]), row[1], HashDigest.from_sql(row[2]) if row[2] is not None else None
+
+    def get_temp_file(self, name) -> Optional[Tuple[int, str]]:
+        row = self.db.execute("SELECT file_id, modified FROM files WHERE name = ? AND temporary = 1;",
+                              (_name_str(temp_name(name)),)).fetchone()
+        return (int(row[0]), row[1]) if row else None
+
+    def get_file_name(self, file_id: int) -> Optional[PurePath]:
+        row = self.db.execute("SELECT name FROM files WHERE file_id = ?;", (file_id,)).fetchone()
+        return PurePath(row[0]) if row else None
+
+    def list_files(self):
+        rows = self.db.execute(
+            "SELECT file_id, name, modified, size, blocks_hash FROM files WHERE temporary = 0;").fetchall()
+        return [(int(r[0]), PurePath(r[1]), r[2], int(r[3] or 0),
+                 HashDigest.from_sql(r[4]) if r[4] is not None else None) for r in rows]
+
+    def list_file_blocks(self, file_id: int) -> List[Tuple[HashDigest, int, int]]:
+        rows = self.db.execute("SELECT hash, offset, size FROM blocks WHERE file_id = ?;", (file_id,)).fetchall()
+        return [(HashDigest.from_sql(r[0]), int(r[1]), int(r[2])) for r in rows]
+
+    def list_temp_files(self) -> List[PurePath]:
+        return [PurePath(r[0]) for r in self.db.execute("SELECT name FROM files WHERE temporary = 1;")]
+
+    def check_temp_files(self):
+        rows = self.db.execute(
+            "SELECT file_id, name, EXISTS (SELECT hash FROM blocks WHERE blocks.file_id = files.file_id "
+            "AND present = 0) AS missing FROM files WHERE temporary = 1;").fetchall()
+        return [(int(r[0]), PurePath(r[1]), bool(r[2])) for r in rows]
+
+    def list_missing_blocks(self) -> List[HashDigest]:
+        return [HashDigest.from_sql(r[0]) for r in self.db.execute("SELECT hash FROM blocks WHERE present = 0;")]
+
+    def list_block_locations(self, hash: HashDigest):
+        rows = self.db.execute(
+            "SELECT files.file_id, files.name, blocks.offset, blocks.size FROM blocks "
+            "INNER JOIN files ON files.file_id = blocks.file_id WHERE hash = ?;", (hash.to_sql(),)).fetchall()
+        return [(int(r[0]), PurePath(r[1]), int(r[2]), int(r[3])) for r in rows]
+
+    # -- mutations (src/index.rs:176-408, 433-451, 591-607)
+    def add_file(self, name, modified: _dt.datetime) -> Tuple[int, bool]:
+        """(file_id, up_to_date): the mtime gate of src/index.rs:176-218."""
+        self.begin()
+        ts = _ts(modified)
+        cur = self.get_file(name)
+        if cur is not None:
+            file_id, old_modified, _ = cur
+            if old_modified != ts:
+                log.info("Resetting file %s, modified", name)
+                self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
+                self.db.execute("UPDATE files SET modified = ?, size = NULL, blocks_hash = NULL, temporary = 0 "
+                                "WHERE file_id = ?;", (ts, file_id))
+                return file_id, False
+            return file_id, True
+        log.info("Inserting new file %s", name)
+        c = self.db.execute("INSERT INTO files(name, modified, temporary) VALUES(?, ?, 0);", (_name_str(name), ts))
+        return int(c.lastrowid), False
+
+    def add_file_overwrite(self, name, modified: _dt.datetime) -> int:
+        self.begin()
+        ts = _ts(modified)
+        cur = self.get_file(name)
+        if cur is not None:
+            file_id = cur[0]
+            self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
+            self.db.execute("UPDATE files SET modified = ?, size = NULL, blocks_hash = NULL, temporary = 0 "
+                            "WHERE file_id = ?;", (ts, file_id))
+            return file_id
+        c = self.db.execute("INSERT INTO files(name, modified, temporary) VALUES(?, ?, 0);", (_name_str(name), ts))
+        return int(c.lastrowid)
+
+    def add_temp_file(self, name) -> int:
+        self.begin()
+        ts = _ts(_dt.datetime.now(_dt.timezone.utc))
+        tname = _name_str(temp_name(name))
+        row = self.db.execute("SELECT file_id FROM files WHERE name = ? AND temporary = 0;", (tname,)).fetchone()
+        if row is not None:
+            file_id = int(row[0])
+            self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
+            self.db.execute("UPDATE files SET modified = ?, size = NULL, blocks_hash = NULL, temporary = 1 "
+                            "WHERE file_id = ?;", (ts, file_id))
+            return file_id
+        c = self.db.execute("INSERT INTO files(name, modified, temporary) VALUES(?, ?, 1);", (tname, ts))
+        return int(c.lastrowid)
+
+    def remove_file(self, file_id: int) -> None:
+        self.begin()
+        self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
+        self.db.execute("DELETE FROM files WHERE file_id = ?;", (file_id,))
+
+    def move_temp_file_into_place(self, file_id: int, destination) -> None:
+        self.begin()
+        dst = _name_str(destination)
+        self.db.execute("DELETE FROM blocks WHERE file_id = (SELECT file_id FROM files WHERE name = ?);", (dst,))
+        self.db.execute("DELETE FROM files WHERE name = ?;", (dst,))
+        self.db.execute("UPDATE files SET name = ?, temporary = 0 WHERE file_id = ?;", (dst, file_id))
+
+    def add_block(self, hash: HashDigest, file_id: int, offset: int, size: int) -> None:
+        """One row, present = 1 (src/index.rs:387-408)."""
+        self.begin()
+        self.db.execute("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);",
+                        (hash.to_sql(), file_id, offset, size))
+
+    def add_blocks(self, file_id: int, rows: Sequence[Tuple[int, int, bytes]]) -> None:
+        """add_block for a whole signature table in one executemany (the
+        reference issues one un-prepared INSERT per block)."""
+        self.begin()
+        self.db.executemany("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);",
+                            ((d.hex(), file_id, o, s) for o, s, d in rows))
+
+    def add_missing_block(self, hash: HashDigest, file_id: int, offset: int, size: int) -> None:
+        self.begin()
+        self.db.execute("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 0);",
+                        (hash.to_sql(), file_id, offset, size))
+
+    def mark_block_present(self, file_id: int, hash: HashDigest, offset: int) -> None:
+        self.begin()
+        self.db.execute("UPDATE blocks SET present = 1 WHERE file_id = ? AND hash = ? AND offset = ?;",
+                        (file_id, hash.to_sql(), offset))
+
+    def set_file_size_and_compute_blocks_hash(self, file_id: int, size: int) -> None:
+        self.begin()
+        bh = self.compute_blocks_hash(file_id)
+        self.db.execute("UPDATE files SET size = ?, blocks_hash = ? WHERE file_id = ?;", (size, bh.to_sql(), file_id))
+
+    def compute_blocks_hash(self, file_id: int) -> HashDigest:
+        """src/index.rs:661-682: SHA-1 over the raw digests, SELECT order."""
+        rows = self.db.execute("SELECT hash FROM blocks WHERE file_id = ?;", (file_id,)).fetchall()
+        raw = b"".join(HashDigest.from_sql(r[0]).bytes for r in rows)
+        return HashDigest(host.blocks_hash(raw))
+
+    # -- the hot path (src/index.rs:610-659)
+    def index_file(self, path, name) -> None:
+        """Cut a file into blocks and add them to the index."""
+        with open(path, "rb") as f:  # File::open first: same error on a missing file
+            file_id, up_to_date = self.add_file(name, _mtime(path))
+            if up_to_date:
+                return
+            if isinstance(self.chunker, FixedChunker):
+                rows_np, _ = host.index_file(path, self.chunker.block_size)
+                rows = host.rows_to_tuples(rows_np)
+            else:
+                rows = signatures_of_bytes(f.read(), self.chunker)
+        for o, s, d in rows:
+            log.debug("Adding block, offset=%d, size=%d, sha1=%s", o, s, d.hex())
+        self.add_blocks(file_id, rows)
+        bh = self.compute_blocks_hash(file_id)
+        self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
+
+    def index_path(self, path) -> None:
+        """Index files and directories recursively (src/index.rs:685-715)."""
+        self._index_path_rec(Path(path), PurePath(""))
+
+    def _index_path_rec(self, root: Path, rel: PurePath) -> None:
+        p = root / rel
+        if p.is_dir():
+            log.info("Indexing directory %s (%s)", rel, p)
+            for entry in sorted(os.listdir(p)):
+                if entry == INDEX_FILE_NAME:
+                    continue
+                self._index_path_rec(root, rel / entry)
+        else:
+            if rel.parts[:1] == (".",):
+                rel = PurePath(*rel.parts[1:])
+            log.info("Indexing file %s (%s)", rel, p)
+            self.index_file(p, rel)
+
+    def remove_missing_files(self, path) -> None:
+        """src/index.rs:718-726."""
+        for file_id, file_path, _m, _s, _bh in self.list_files():
+            if not (Path(path) / file_path).is_file():
+                log.info("Removing missing file %s", file_path)
+                self.remove_file(file_id)

@@ -1,0 +1,166 @@
+"""The reference library API (Index, HashDigest) on top of the C-ABI.
+
+CPU tests mirror the reference's own unit tests (src/lib.rs:184-213) and the
+SQLite row semantics of src/index.rs; GPU tests mirror the index KAT
+(src/index.rs:747-793) with the reference's boundaries, and index a directory
+with fixed-size blocks against the oracle."""
+import datetime as dt
+import hashlib
+import os
+from pathlib import PurePath
+
+import numpy as np
+import pytest
+
+import oracle
+from syncfast_amd.digest import HashDigest, InvalidHashDigest
+from syncfast_amd.index import BoundaryChunker, FixedChunker, Index, temp_name, untemp_name
+
+T0 = dt.datetime(2020, 1, 2, 3, 4, 5, tzinfo=dt.timezone.utc)
+
+
+# ---- src/lib.rs:184-213 ---------------------------------------------------
+
+def test_hash_tosql():
+    d = HashDigest(hashlib.sha1(b"test").digest())
+    assert d.to_sql() == "a94a8fe5ccb19ba61c4c0873d391e987982fbbd3"
+    assert str(d) == d.to_sql()
+
+
+def test_hash_fromsql():
+    d = HashDigest(hashlib.sha1(b"test").digest())
+    assert HashDigest.from_sql("a94a8fe5ccb19ba61c4c0873d391e987982fbbd3") == d
+    assert HashDigest.from_sql("A94A8FE5CCB19BA61C4C0873D391E987982FBBD3") == d
+    with pytest.raises(InvalidHashDigest, match="wrong size"):
+        HashDigest.from_sql("a94a")
+    with pytest.raises(InvalidHashDigest, match="invalid character"):
+        HashDigest.from_sql("zz4a8fe5ccb19ba61c4c0873d391e987982fbbd3")
+    with pytest.raises(InvalidHashDigest, match="invalid character"):
+        HashDigest.from_sql(" 94a8fe5ccb19ba61c4c0873d391e987982fbbd3")
+
+
+def test_temp_name():
+    assert temp_name("file") == PurePath(".syncfast_tmp_file")
+    assert temp_name("dir/file") == PurePath("dir/.syncfast_tmp_file")
+    assert untemp_name("dir/.syncfast_tmp_file") == PurePath("dir/file")
+
+
+# ---- src/index.rs rows and queries (no GPU) --------------------------------
+
+def test_schema_and_pragmas(tmp_path):
+    idx = Index.open(tmp_path / "x.idx")
+    assert idx.db.execute("PRAGMA application_id").fetchone()[0] == 0x51367457
+    tables = {r[0] for r in idx.db.execute("SELECT name FROM sqlite_master WHERE type='table'")}
+    assert tables == {"files", "blocks"}
+    idx2 = Index.open(tmp_path / "x.idx")  # existing file: schema not re-created
+    assert idx2.list_files() == []
+
+
+def test_add_file_mtime_gate_and_blocks():
+    idx = Index.open_in_memory()
+    fid, up = idx.add_file("dir/name", T0)
+    assert (fid, up) == (1, False)
+    digs = [hashlib.sha1(bytes([i])).digest() for i in range(3)]
+    idx.add_blocks(fid, [(0, 10, digs[0]), (10, 10, digs[1])])
+    idx.add_block(HashDigest(digs[2]), fid, 20, 5)
+    assert idx.add_file("dir/name", T0) == (1, True)
+    assert idx.get_block(HashDigest(digs[1])) == (PurePath("dir/name"), 10, 10)
+    assert idx.get_block(HashDigest(b"12345678901234567890")) is None
+    bh = idx.compute_blocks_hash(fid)
+    assert bh.bytes == hashlib.sha1(b"".join(digs)).digest()
+    # size stays NULL through index_file-style inserts -> list_files reports 0
+    assert idx.list_files()[0][3] == 0
+    idx.set_file_size_and_compute_blocks_hash(fid, 25)
+    assert idx.list_files()[0][3] == 25 and idx.list_files()[0][4] == bh
+    # modified time changed -> blocks dropped, not up to date
+    assert idx.add_file("dir/name", T0 + dt.timedelta(seconds=1)) == (1, False)
+    assert idx.list_file_blocks(1) == []
+    idx.commit()
+
+
+def test_missing_blocks_and_temp_files():
+    idx = Index.open_in_memory()
+    tid = idx.add_temp_file("a/b")
+    assert idx.list_temp_files() == [PurePath("a/.syncfast_tmp_b")]
+    h = HashDigest(hashlib.sha1(b"x").digest())
+    idx.add_missing_block(h, tid, 0, 1)
+    assert idx.list_missing_blocks() == [h]
+    assert idx.check_temp_files() == [(tid, PurePath("a/.syncfast_tmp_b"), True)]
+    assert idx.get_block(h) is None  # present = 0
+    idx.mark_block_present(tid, h, 0)
+    assert idx.check_temp_files()[0][2] is False
+    assert idx.list_block_locations(h) == [(tid, PurePath("a/.syncfast_tmp_b"), 0, 1)]
+    idx.move_temp_file_into_place(tid, "a/b")
+    assert idx.get_file("a/b")[0] == tid and idx.list_temp_files() == []
+    idx.remove_file(tid)
+    assert idx.list_files() == []
+
+
+# ---- GPU: the hot path inside Index.index_file ----------------------------
+
+KAT_SIZES = [11579, 32768, 546]  # src/index.rs:771,778,785
+
+
+@pytest.mark.gpu
+def test_reference_index_kat(gpu, tmp_path):
+    """src/index.rs:747-793 with the reference's block boundaries."""
+    p = tmp_path / "kat"
+    p.write_bytes(oracle.kat_input())
+    name = PurePath("dir/name")
+    index = Index.open_in_memory(chunker=BoundaryChunker(lambda data: KAT_SIZES))
+    index.index_file(p, name)
+    index.commit()
+    assert index.get_block(HashDigest(b"12345678901234567890")) is None
+    block1 = index.get_block(HashDigest(bytes.fromhex("fb5ef7ebadd82c8085c5ff63823622bae0e263f6")))
+    assert block1 == (name, 0, 11579)
+    block2 = index.get_block(HashDigest(bytes.fromhex("570d8b30fcfd585e4127b561f5ecd376ff4d0101")))
+    assert block2 == (name, 11579, 32768)
+    block3 = index.get_block(HashDigest(bytes.fromhex("b9a8c2641af2cf8fd8f36a2456a3eaa95c029127")))
+    assert block3 == (name, 44347, 546)
+    assert block3[1] - block2[1] == 1 << 15  # MAX_BLOCK_SIZE
+    file1 = index.get_file(name)
+    assert file1[0] == 1
+    assert file1[2] == HashDigest(bytes.fromhex("84c25d78edcdb67631639c43604cf0149564f044"))
+
+
+@pytest.mark.gpu
+def test_index_path_fixed_blocks(gpu, tmp_path):
+    root = tmp_path / "tree"
+    (root / "sub").mkdir(parents=True)
+    files = {"a.bin": 100_000, "sub/b.bin": 4096 * 3, "sub/empty": 0, "c": 1}
+    for i, (n, ln) in enumerate(files.items()):
+        (root / n).write_bytes(oracle.splitmix_bytes(ln, 1000 + i).tobytes())
+    idx = Index.open(root / ".syncfast.idx", chunker=FixedChunker(4096))
+    idx.index_path(root)
+    idx.remove_missing_files(root)
+    idx.commit()
+    names = {str(f[1]) for f in idx.list_files()}
+    assert names == set(files)  # the index file itself is skipped
+    for i, (n, ln) in enumerate(files.items()):
+        fid, _, bh = idx.get_file(n)
+        data = oracle.splitmix_bytes(ln, 1000 + i)
+        offs, sizes, want = oracle.index_fixed(data, 4096)
+        got = idx.list_file_blocks(fid)
+        assert [(g[0].bytes, g[1], g[2]) for g in got] == [(bytes(w), int(o), int(s)) for w, o, s in zip(want, offs, sizes)]
+        assert bh.bytes == oracle.blocks_hash(want)
+    # unchanged mtimes -> nothing re-indexed; a touched file is re-indexed
+    before = idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0]
+    os.utime(root / "c", ns=(1, 1))
+    idx.index_path(root)
+    idx.commit()
+    assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
+    os.remove(root / "sub" / "b.bin")
+    idx.remove_missing_files(root)
+    idx.commit()
+    assert "sub/b.bin" not in {str(f[1]) for f in idx.list_files()}
+
+
+@pytest.mark.gpu
+def test_boundary_chunker_random(gpu):
+    rng = np.random.default_rng(5)
+    data = oracle.splitmix_bytes(200_000, 77).tobytes()
+    cuts = sorted(set(int(x) for x in rng.integers(1, len(data), 40)))
+    sizes = np.diff([0] + cuts + [len(data)]).tolist()
+    from syncfast_amd.index import signatures_of_bytes
+    rows = signatures_of_bytes(data, BoundaryChunker(lambda d: sizes))
+    assert [r[2] for r in rows] == oracle.py_index_blocks(data, [r[0] for r in rows], sizes)
