@@ -324,11 +324,66 @@ int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t s
   return hip_err(hipGetLastError());
 }
 
+// Host buffer that is (or was made) page-locked: the DMA engine reads it in
+// place, stage by stage, overlapped with the kernel of the previous stage.
+static int index_registered(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
+                     uint64_t* n_out) {
+  const uint64_t nblocks = ceil_div(len, bs);
+  if (n_out) *n_out = nblocks;
+  if (nblocks > cap) return SF_ENOSPC;
+  const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
+  const uint64_t nstages = ceil_div(len, stage);
+  Streams st;
+  DevBuf ddata[2], ddig;
+  PinBuf pdig;
+  for (int i = 0; i < 2; i++) {
+    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
+    SF_HIP(hipMalloc(&ddata[i].p, stage));
+  }
+  SF_HIP(hipMalloc(&ddig.p, nblocks * 20));
+  SF_HIP(hipHostMalloc(&pdig.p, nblocks * 20, hipHostMallocDefault));
+  int rc = SF_OK;
+  for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    const uint64_t off = k * stage;
+    const uint64_t n = std::min(stage, len - off);
+    // stream b is in order: the copy into ddata[b] waits for the kernel of
+    // stage k-2 that read it.
+    if (hipMemcpyAsync(ddata[b].p, data + off, n, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+    rc = launch_fixed(ddata[b].p, n, bs, ceil_div(n, bs), static_cast<uint8_t*>(ddig.p) + (off / bs) * 20, st.s[b]);
+  }
+  for (int i = 0; i < 2; i++)
+    if (hipStreamSynchronize(st.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
+  for (uint64_t i = 0; i < nblocks; i++) {
+    out[i].offset = i * bs;
+    out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
+    memcpy(out[i].sha1, dg + 20 * i, 20);
+  }
+  return SF_OK;
+}
+
 int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
   int rc = check_fixed_args(len, block_size);
   if (rc) return rc;
   if (len && (!data || !out)) return SF_EINVAL;
+  // Large buffers: page-lock in place (no staging memcpy); SF_NO_HOSTREG=1
+  // forces the staged path (A/B knob).
+  const char* noreg = getenv("SF_NO_HOSTREG");
+  if (len >= (64ull << 20) && !(noreg && atoi(noreg))) {
+    if (hipHostRegister(const_cast<uint8_t*>(data), len, hipHostRegisterReadOnly) == hipSuccess) {
+      rc = index_registered(data, len, block_size, out, cap, n_out);
+      (void)hipHostUnregister(const_cast<uint8_t*>(data));
+      return rc;
+    }
+    (void)hipGetLastError();
+  }
   return index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
     memcpy(dst, data + off, n);
     return SF_OK;
