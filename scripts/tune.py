@@ -1,7 +1,7 @@
 """Interleaved A/B of kernel variants in ONE process (cdna guide rule 24).
 
 Variants are selected per call through env knobs read by the C-ABI
-(SF_TILE).  Reports median / min ms per launch over rounds and checks that
+(SF_VARIANT: 0 shipped = <128,1>, 1 = <128,5>, 2 = <64,6>, 3 = <64,8>, 4 = <64,1>).  Reports median / min ms per launch over rounds and checks that
 every variant produces identical digests."""
 import os
 import statistics
@@ -19,7 +19,7 @@ GiB = 1 << 30
 def main():
     size = int(float(os.environ.get("TUNE_GIB", "8")) * GiB)
     bs = int(os.environ.get("TUNE_BS", "4096"))
-    variants = [dict(SF_TILE=t) for t in os.environ.get("TUNE_TILES", "128,64").split(",")]
+    variants = [dict(SF_VARIANT=t) for t in os.environ.get("TUNE_VARIANTS", "0,1,2,3,4").split(",")]
     rounds, reps = 5, 5
     data = device.splitmix_tensor(size, 0x5EED0000)
     outs = {}

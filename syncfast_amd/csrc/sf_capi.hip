@@ -23,11 +23,12 @@ namespace {
 
 constexpr int kTile = 128;  // bytes of each block staged per LDS step
 
-// Tuning knob for experiments (interleaved A/B in one process): SF_TILE=64
-// selects the 64-B staging variant.  Read on every call.
-inline int tile_choice() {
-  const char* e = getenv("SF_TILE");
-  return (e && atoi(e) == 64) ? 64 : kTile;
+// Tuning knob for experiments (interleaved A/B in one process): SF_VARIANT
+// selects a (tile, waves-per-SIMD) build of the fixed kernel; 0 = shipped.
+// Read on every call.
+inline int variant_choice() {
+  const char* e = getenv("SF_VARIANT");
+  return e ? atoi(e) : 0;
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -77,12 +78,15 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   if (nblocks == 0) return SF_OK;
   const unsigned grid = grid_for_blocks(nblocks);
   const sf::PadSchedule pad = pad_schedule(bs);
-  if (tile_choice() == 64)
-    hipLaunchKernelGGL(sf::sha1_fixed_kernel<64>, dim3(grid), dim3(sf::kThreads), 0, stream,
-                       static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests), pad);
-  else
-    hipLaunchKernelGGL(sf::sha1_fixed_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
-                       static_cast<const uint8_t*>(d_data), len, bs, nblocks, static_cast<uint8_t*>(d_digests), pad);
+  const uint8_t* d = static_cast<const uint8_t*>(d_data);
+  uint8_t* o = static_cast<uint8_t*>(d_digests);
+  switch (variant_choice()) {
+    case 1: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 5>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 3: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 8>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+  }
   return hip_err(hipGetLastError());
 }
 

@@ -129,7 +129,7 @@ struct WaveGeo {
 // and covers the rest of the span, so lanes past the span read zeros.
 template <int TILE>
 __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t span, uint32_t step,
-                                           const uint32_t (&voff)[TILE / 16], uint4* wave_tile) {
+                                           const uint32_t* voff, uint4* wave_tile) {
   // All operands are wave-uniform; readfirstlane keeps the resource in SGPRs
   // (a VGPR resource makes hipcc wrap every DMA in a waterfall loop).
   const uint64_t toff = (uint64_t)step * TILE;
@@ -146,10 +146,10 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
 // Hash the block (off, size) owned by this lane; all 64 lanes of the wave
 // enter together.  `rel` = off - geo.base (valid lanes).  TILE = bytes of
 // each block staged per LDS step.
-template <int TILE>
+template <int TILE, bool HAS_PAD>
 __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
                                           uint32_t rel, bool valid, const WaveGeo& geo,
-                                          uint4* __restrict__ wave_tile, Sha1& st, const PadSchedule* pad) {
+                                          uint4* __restrict__ wave_tile, Sha1& st, const PadSchedule pad) {
   constexpr int PIECES = TILE / 16;           // 16-B pieces per block per step
   constexpr int CH = TILE / 64;               // compressions per step
   constexpr int GSHIFT = PIECES == 4 ? 2 : (PIECES == 8 ? 1 : 0);
@@ -215,8 +215,10 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
   }
   // Every block of the wave has the same 64-B multiple size and all its data
   // chunks are done: the last chunk is the same padding for every lane.
-  if (pad && pad->bytes == geo.min_size && geo.min_size == geo.max_size && c_done == nfull) {
-    st.compress_uniform(pad->kw);
+  // (pad is passed by value, never by address: a kernel argument whose
+  // address escapes is copied to scratch.)
+  if (HAS_PAD && pad.bytes == geo.min_size && geo.min_size == geo.max_size && c_done == nfull) {
+    st.compress_uniform(pad.kw);
     return;
   }
   // Remaining data chunks and the padding chunk(s), per lane.
@@ -233,8 +235,10 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 // ---------------------------------------------------------------- kernels
 
 // Fixed tiling: block i = data[i*bs, min((i+1)*bs, len)).
-template <int TILE>
-__global__ void __launch_bounds__(kThreads)
+// WPE = minimum resident waves per SIMD requested from the register
+// allocator (__launch_bounds__ 2nd argument, per EU on gfx950).
+template <int TILE, int WPE = 1>
+__global__ void __launch_bounds__(kThreads, WPE)
 sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
                   uint8_t* __restrict__ digests, const PadSchedule pad) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
@@ -260,7 +264,7 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   const uint32_t rel = (uint32_t)((uint64_t)lane * bs);
 
   Sha1 st;
-  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, &pad);
+  hash_wave<TILE, true>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
   if (valid) st.store(digests + blk * 20);
 }
 
@@ -307,7 +311,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 
   Sha1 st;
-  hash_wave<TILE>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, nullptr);
+  hash_wave<TILE, false>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, PadSchedule{});
   if (valid) {
     if (bad) {
       uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);
