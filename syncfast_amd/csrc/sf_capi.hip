@@ -260,6 +260,22 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   if (n_files == 0) return SF_OK;
   if (!d_data || (total && !d_digests)) return SF_EINVAL;
 
+  // Equal-size, block-aligned, back-to-back files: the block table is a fixed
+  // tiling of the batch, and each file's digest run is a fixed tiling of the
+  // digest table (block = nbf*20 bytes), so nothing needs uploading.
+  bool equal_files = contiguous_aligned && total > 0;
+  for (uint32_t f = 1; f < n_files && equal_files; f++)
+    if (files[f].len != files[0].len) equal_files = false;
+  if (equal_files && total / n_files * 20 <= SF_MAX_BLOCK_SIZE) {
+    const uint64_t nbf = total / n_files;
+    const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
+    rc = launch_fixed(base, total * (uint64_t)block_size, block_size, total, d_digests, s);
+    if (rc) return rc;
+    if (d_file_hashes)
+      rc = launch_fixed(d_digests, total * 20, (uint32_t)(nbf * 20), n_files, d_file_hashes, s);
+    return rc;
+  }
+
   // Block table for the ragged case, file table for blocks_hash; one device
   // workspace, uploaded once.
   const bool need_table = !contiguous_aligned && total > 0;

@@ -1,0 +1,55 @@
+"""GPU parity at BASELINE sizes.
+
+configs[1]: 8 GiB in 4 KiB blocks -- every one of the 2^21 digests compared
+with the multi-threaded C oracle on the host (bit-exact, plus blocks_hash).
+configs[4]: 32 GiB in 64 KiB blocks -- size-independent properties: a
+random sample of blocks vs the oracle, the last block, idempotence of a second
+launch, and the chunked-vs-whole checksum of checksums."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from syncfast_amd import device, host
+
+pytestmark = pytest.mark.gpu
+GiB = 1 << 30
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def test_config2_8gib_4k_every_digest(gpu):
+    n, bs = 8 * GiB, 4096
+    data = device.splitmix_tensor(n, 0x5EED0000, gpu)
+    dig = device.index_device(data, bs).cpu().numpy()
+    host_bytes = data.cpu().numpy()
+    del data
+    torch.cuda.empty_cache()
+    want = oracle.index_fixed_mt(host_bytes, bs, _threads())
+    assert dig.shape == (n // bs, 20)
+    bad = np.nonzero((dig != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} digests differ, first at block {bad[:5]}"
+    assert host.blocks_hash(dig) == oracle.blocks_hash(want)
+
+
+def test_config5_32gib_64k_properties(gpu):
+    n, bs = 32 * GiB, 65536
+    data = device.splitmix_tensor(n, 0x5EED0004, gpu)
+    d1 = device.index_device(data, bs)
+    d2 = device.index_device(data, bs)
+    assert torch.equal(d1, d2)  # idempotent
+    dig = d1.cpu().numpy()
+    rng = np.random.default_rng(4)
+    sample = np.unique(np.concatenate([rng.integers(0, n // bs, 600), [0, 63, 64, n // bs - 1]]))
+    for i in sample:
+        blk = data[i * bs:(i + 1) * bs].cpu().numpy()
+        assert bytes(dig[i]) == oracle.sha1(blk), i
+    # checksum of checksums: indexing the halves separately gives the same table
+    half = n // 2
+    h1 = device.index_device(data[:half], bs)
+    h2 = device.index_device(data[half:], bs)
+    assert host.blocks_hash(torch.cat([h1, h2]).cpu().numpy()) == host.blocks_hash(dig)
