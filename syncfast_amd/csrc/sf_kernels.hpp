@@ -181,12 +181,19 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 
     if (nsteps > 0) issue_step<TILE>(span_ptr, geo.span, 0, voff, wave_tile);
     for (uint32_t t = 0; t < nsteps; ++t) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       uint4 raw[PIECES];
+#ifndef SF_EXPERIMENT_NOLOAD
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < PIECES; ++k) raw[k] = my[k ^ g];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t + 1 < nsteps) issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+#else
+      // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_NOLOAD):
+      // same VALU work on register data, no loads -- isolates compute cost.
+#pragma unroll
+      for (int k = 0; k < PIECES; ++k) raw[k] = make_uint4(rel ^ (t * 977u + k), t + k, rel + k, voff[k & 7]);
+#endif
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
         uint32_t w[16];
