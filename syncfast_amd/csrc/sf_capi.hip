@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../../include/syncfast_amd.h"
@@ -98,6 +99,60 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
                      static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
                      static_cast<uint8_t*>(d_digests), d_status);
   return hip_err(hipGetLastError());
+}
+
+// A second stream per device for the per-file blocks_hash chains of the
+// staged batch (created once, kept for the process lifetime).
+hipStream_t side_stream(int* rc) {
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { *rc = SF_ENODEV; return nullptr; }
+  std::lock_guard<std::mutex> g(mu);
+  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
+    *rc = SF_ENODEV;
+    return nullptr;
+  }
+  *rc = SF_OK;
+  return streams[dev];
+}
+
+// Many equal-size, block-aligned files back to back: hash the blocks in S
+// column stages (stage k = blocks [k*m, (k+1)*m) of every file) on `s`; after
+// each stage, advance every file's blocks_hash chain over that stage's
+// digests on the side stream.  Only the last stage's chains stay exposed.
+int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
+                 uint8_t* fh, hipStream_t s) {
+  int rc = SF_OK;
+  hipStream_t side = side_stream(&rc);
+  if (rc) return rc;
+  int S = 1;
+  for (int cand : {8, 4, 2})
+    if (nbf % (16ull * cand) == 0 && nbf / cand >= 64) { S = cand; break; }
+  const uint64_t m = nbf / S;
+  const sf::PadSchedule pad = pad_schedule(bs);
+  uint32_t* state = nullptr;
+  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&state), (size_t)nfiles * 20, s));
+  std::vector<hipEvent_t> ev(S + 1, nullptr);
+  for (auto& e : ev) SF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const unsigned cgrid = (unsigned)ceil_div(nfiles, 64);
+  for (int k = 0; k < S && rc == SF_OK; k++) {
+    const uint64_t nb = (uint64_t)nfiles * m;
+    hipLaunchKernelGGL(sf::sha1_grid_kernel<kTile>, dim3(grid_for_blocks(nb)), dim3(sf::kThreads), 0, s,
+                       base + k * m * bs, bs, (uint64_t)nfiles, m, flen, dig + k * m * 20, nbf, pad);
+    rc = hip_err(hipGetLastError());
+    if (rc) break;
+    if (hipEventRecord(ev[k], s) != hipSuccess || hipStreamWaitEvent(side, ev[k], 0) != hipSuccess) { rc = SF_ENODEV; break; }
+    hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3(cgrid), dim3(64), 0, side, dig, nbf * 20, nfiles,
+                       (uint32_t)(nbf * 20), (uint32_t)(k * m * 20), (uint32_t)((k + 1) * m * 20), state, fh,
+                       k == 0 ? 1 : 0, k == S - 1 ? 1 : 0);
+    rc = hip_err(hipGetLastError());
+  }
+  // The caller's stream resumes after the last chain; then free the state.
+  if (hipEventRecord(ev[S], side) != hipSuccess || hipStreamWaitEvent(s, ev[S], 0) != hipSuccess) rc = rc ? rc : SF_ENODEV;
+  (void)hipFreeAsync(state, s);
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc;
 }
 
 int check_fixed_args(uint64_t len, uint32_t bs) {
@@ -266,14 +321,13 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   bool equal_files = contiguous_aligned && total > 0;
   for (uint32_t f = 1; f < n_files && equal_files; f++)
     if (files[f].len != files[0].len) equal_files = false;
-  if (equal_files && total / n_files * 20 <= SF_MAX_BLOCK_SIZE) {
+  if (equal_files && total / n_files * 20 <= 0xFFFFFFFFull) {
     const uint64_t nbf = total / n_files;
     const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
-    rc = launch_fixed(base, total * (uint64_t)block_size, block_size, total, d_digests, s);
-    if (rc) return rc;
-    if (d_file_hashes)
-      rc = launch_fixed(d_digests, total * 20, (uint32_t)(nbf * 20), n_files, d_file_hashes, s);
-    return rc;
+    if (!d_file_hashes)
+      return launch_fixed(base, total * (uint64_t)block_size, block_size, total, d_digests, s);
+    return batch_staged(base, files[0].len, block_size, n_files, nbf, static_cast<uint8_t*>(d_digests),
+                        static_cast<uint8_t*>(d_file_hashes), s);
   }
 
   // Block table for the ragged case, file table for blocks_hash; one device

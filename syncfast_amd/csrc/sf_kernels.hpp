@@ -275,6 +275,98 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   if (valid) st.store(digests + blk * 20);
 }
 
+// Row-major grid of full-size blocks: `rows` files, `cols` blocks of each
+// (one column range of a many-file batch).  Block b = (row b / cols,
+// col b % cols) reads data[row*in_stride + col*bs, +bs) and writes digest
+// out[row*out_stride + col].  Used by the staged many-file batch, which
+// hashes each file's blocks in column stages so that the per-file
+// blocks_hash chains can advance on a second stream.
+template <int TILE>
+__global__ void __launch_bounds__(kThreads)
+sha1_grid_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols,
+                 uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nblocks = rows * cols;
+  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
+  if (first >= nblocks) return;
+  const uint64_t blk = first + lane;
+  const bool valid = blk < nblocks;
+  const uint64_t b = valid ? blk : first;
+  const uint64_t row = b / cols, col = b - row * cols;
+  const uint64_t off = row * in_stride + col * bs;
+  const uint64_t last = (first + 64 <= nblocks) ? first + 63 : nblocks - 1;
+  const uint64_t r0 = first / cols, r1 = last / cols;
+  WaveGeo geo;
+  geo.base = r0 * in_stride + (first - r0 * cols) * bs;
+  geo.span = r1 * in_stride + (last - r1 * cols) * bs + bs - geo.base;
+  geo.min_size = bs;
+  geo.max_size = bs;
+  geo.max_nch = n_chunks(bs);
+  geo.lds_ok = ((bs & 15u) == 0) && ((in_stride & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
+               geo.span < 0xF0000000ull;
+  const uint32_t rel = (uint32_t)(off - geo.base);
+  Sha1 st;
+  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
+  if (valid) st.store(digests + (row * out_stride + col) * 20);
+}
+
+// One lane per file: advance the file's blocks_hash SHA-1 (src/index.rs:
+// 661-682) over bytes [lo, hi) of its digest run (hi - lo a multiple of 64),
+// keeping the chaining state in `state` (5 words per file) between stages;
+// `last` also hashes the rest of the run plus the padding and writes the
+// 20-byte blocks_hash.  The next chunk's loads are issued before the current
+// compression, since each chain is latency bound (one lane, one wave).
+__global__ void __launch_bounds__(64)
+sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
+                  uint32_t lo, uint32_t hi, uint32_t* __restrict__ state, uint8_t* __restrict__ out, int first,
+                  int last) {
+  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+  if (f >= nfiles) return;
+  Sha1 st;
+  if (first) st.init();
+  else {
+    st.h0 = state[5 * f]; st.h1 = state[5 * f + 1]; st.h2 = state[5 * f + 2];
+    st.h3 = state[5 * f + 3]; st.h4 = state[5 * f + 4];
+  }
+  const uint8_t* p = runs + (uint64_t)f * run_stride;
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint32_t c = lo;
+  if (c + 64 <= hi) {
+    uint4 cur[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] = q[c / 16 + j];
+    for (; c + 64 <= hi; c += 64) {
+      uint4 nxt[4];
+      const bool more = c + 128 <= hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nxt[j] = more ? q[(c + 64) / 16 + j] : cur[j];
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w[4 * j] = bswap32(cur[j].x); w[4 * j + 1] = bswap32(cur[j].y);
+        w[4 * j + 2] = bswap32(cur[j].z); w[4 * j + 3] = bswap32(cur[j].w);
+      }
+      st.compress(w);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
+  }
+  if (!last) {
+    state[5 * f] = st.h0; state[5 * f + 1] = st.h1; state[5 * f + 2] = st.h2;
+    state[5 * f + 3] = st.h3; state[5 * f + 4] = st.h4;
+    return;
+  }
+  const uint32_t nch = n_chunks(run_len);
+  for (uint32_t k = c / 64; k < nch; ++k) {
+    uint32_t w[16];
+    build_tail_chunk(w, p, run_len, k, nch);
+    st.compress(w);
+  }
+  st.store(out + (uint64_t)f * 20);
+}
+
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
 // Used for content-defined boundaries, the reference KAT boundaries, ragged
 // many-file batches, and (over the digest table) per-file blocks_hash.

@@ -199,3 +199,18 @@ def test_block_digest_independent_of_neighbours(gpu):
     ref = oracle.sha1(blk)
     for i in (0, 63, 64, 65, 127, 199):
         assert bytes(d[i]) == ref
+
+
+@pytest.mark.parametrize("nfiles,nbf", [(64, 1024), (3, 256), (130, 64)])
+def test_batch_staged_chains(gpu, nfiles, nbf):
+    # equal-size contiguous files: column stages + per-file chains on a side stream
+    bs = 4096
+    data = oracle.splitmix_bytes(nfiles * nbf * bs, 95 + nbf)
+    t = to_dev(data.tobytes(), gpu)
+    files = [(i * nbf * bs, nbf * bs) for i in range(nfiles)]
+    dig, first, fh = device.index_device_batch(t, files, bs)
+    want = oracle.index_fixed_mt(data, bs, 8)
+    assert np.array_equal(dig.cpu().numpy(), want)
+    fhn = fh.cpu().numpy()
+    for i in range(nfiles):
+        assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
