@@ -127,8 +127,10 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   hipStream_t side = side_stream(&rc);
   if (rc) return rc;
   int S = 1;
-  for (int cand : {8, 4, 2})
-    if (nbf % (16ull * cand) == 0 && nbf / cand >= 64) { S = cand; break; }
+  const char* se = getenv("SF_STAGES");  // A/B knob; default: the most stages up to 8
+  const int smax = se ? std::max(1, atoi(se)) : 8;
+  for (int cand : {16, 8, 4, 2})
+    if (cand <= smax && nbf % (16ull * cand) == 0 && nbf / cand >= 64) { S = cand; break; }
   const uint64_t m = nbf / S;
   const sf::PadSchedule pad = pad_schedule(bs);
   uint32_t* state = nullptr;
