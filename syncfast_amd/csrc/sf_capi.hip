@@ -117,42 +117,53 @@ hipStream_t side_stream(int* rc) {
   return streams[dev];
 }
 
-// Many equal-size, block-aligned files back to back: hash the blocks in S
-// column stages (stage k = blocks [k*m, (k+1)*m) of every file) on `s`; after
-// each stage, advance every file's blocks_hash chain over that stage's
-// digests on the side stream.  Only the last stage's chains stay exposed.
+// Many equal-size, block-aligned files back to back.  ONE launch hashes the
+// blocks in S column stages (stage k = blocks [k*m, (k+1)*m) of every file,
+// stage-major) and publishes per-stage arrival counters; the per-file
+// blocks_hash chains run concurrently on the side stream and consume each
+// stage as soon as it is complete.  Only the last stage's chains stay
+// exposed after the block hashing.  The side stream starts after the
+// counters are zeroed (event after the memset), and the caller's stream
+// resumes after the chains.
 int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
                  uint8_t* fh, hipStream_t s) {
   int rc = SF_OK;
   hipStream_t side = side_stream(&rc);
   if (rc) return rc;
   int S = 1;
-  const char* se = getenv("SF_STAGES");  // A/B knob; default: the most stages up to 8
-  const int smax = se ? std::max(1, atoi(se)) : 8;
-  for (int cand : {16, 8, 4, 2})
-    if (cand <= smax && nbf % (16ull * cand) == 0 && nbf / cand >= 64) { S = cand; break; }
+  const char* se = getenv("SF_STAGES");  // A/B knob; default up to 16 stages
+  const int smax = se ? std::max(1, atoi(se)) : 16;
+  for (int cand : {32, 16, 8, 4, 2})
+    if (cand <= smax && nbf % (64ull * cand) == 0 && ((uint64_t)nfiles * (nbf / cand)) % 64 == 0) {
+      S = cand;
+      break;
+    }
   const uint64_t m = nbf / S;
+  const uint64_t per_stage = (uint64_t)nfiles * m;
+  const bool staged = S > 1;
   const sf::PadSchedule pad = pad_schedule(bs);
-  uint32_t* state = nullptr;
-  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&state), (size_t)nfiles * 20, s));
-  std::vector<hipEvent_t> ev(S + 1, nullptr);
+  uint32_t* words = nullptr;  // [0, 32): stage counters, [32]: timeout word; 16-B padded block
+  const size_t wbytes = 48 * sizeof(uint32_t);
+  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
+  SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
+  hipEvent_t ev[2] = {nullptr, nullptr};
   for (auto& e : ev) SF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  const unsigned cgrid = (unsigned)ceil_div(nfiles, 64);
-  for (int k = 0; k < S && rc == SF_OK; k++) {
-    const uint64_t nb = (uint64_t)nfiles * m;
-    hipLaunchKernelGGL(sf::sha1_grid_kernel<kTile>, dim3(grid_for_blocks(nb)), dim3(sf::kThreads), 0, s,
-                       base + k * m * bs, bs, (uint64_t)nfiles, m, flen, dig + k * m * 20, nbf, pad);
-    rc = hip_err(hipGetLastError());
-    if (rc) break;
-    if (hipEventRecord(ev[k], s) != hipSuccess || hipStreamWaitEvent(side, ev[k], 0) != hipSuccess) { rc = SF_ENODEV; break; }
-    hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3(cgrid), dim3(64), 0, side, dig, nbf * 20, nfiles,
-                       (uint32_t)(nbf * 20), (uint32_t)(k * m * 20), (uint32_t)((k + 1) * m * 20), state, fh,
-                       k == 0 ? 1 : 0, k == S - 1 ? 1 : 0);
-    rc = hip_err(hipGetLastError());
-  }
-  // The caller's stream resumes after the last chain; then free the state.
-  if (hipEventRecord(ev[S], side) != hipSuccess || hipStreamWaitEvent(s, ev[S], 0) != hipSuccess) rc = rc ? rc : SF_ENODEV;
-  (void)hipFreeAsync(state, s);
+  do {
+    if (hipEventRecord(ev[0], s) != hipSuccess) { rc = SF_ENODEV; break; }
+    const uint64_t nb = (uint64_t)nfiles * nbf;
+    hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid_for_blocks(nb)), dim3(sf::kThreads), 0, s, base, bs,
+                       (uint64_t)nfiles, nbf, m, flen, dig, nbf, pad, words);
+    if ((rc = hip_err(hipGetLastError()))) break;
+    // Unstaged: the chains simply follow the block kernel on the side stream.
+    if (hipStreamWaitEvent(side, ev[0], 0) != hipSuccess) { rc = SF_ENODEV; break; }
+    if (!staged && hipEventRecord(ev[1], s) == hipSuccess) (void)hipStreamWaitEvent(side, ev[1], 0);
+    hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3((unsigned)ceil_div(nfiles, 64)), dim3(64), 0, side, dig, nbf * 20,
+                       nfiles, (uint32_t)(nbf * 20), (uint32_t)S, (uint32_t)(m * 20),
+                       staged ? words : nullptr, (uint32_t)(per_stage / 64), fh, words + 32);
+    if ((rc = hip_err(hipGetLastError()))) break;
+    if (hipEventRecord(ev[1], side) != hipSuccess || hipStreamWaitEvent(s, ev[1], 0) != hipSuccess) rc = SF_ENODEV;
+  } while (0);
+  (void)hipFreeAsync(words, s);
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
 }

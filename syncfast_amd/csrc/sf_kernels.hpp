@@ -275,32 +275,40 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   if (valid) st.store(digests + blk * 20);
 }
 
-// Row-major grid of full-size blocks: `rows` files, `cols` blocks of each
-// (one column range of a many-file batch).  Block b = (row b / cols,
-// col b % cols) reads data[row*in_stride + col*bs, +bs) and writes digest
-// out[row*out_stride + col].  Used by the staged many-file batch, which
-// hashes each file's blocks in column stages so that the per-file
-// blocks_hash chains can advance on a second stream.
+// Many equal-size files, blocks hashed in column stages inside ONE launch.
+// `rows` files of `cols` full-size blocks; stage k = columns [k*m, (k+1)*m)
+// of every file, blocks numbered stage-major (stage, row, column), so the
+// dispatcher finishes stage k's waves roughly before stage k+1's.  Block
+// (row, col) reads data[row*in_stride + col*bs, +bs) and writes digest
+// out[row*out_stride + col].  After storing its 64 digests each wave
+// publishes (release, agent scope) one arrival on stage_done[stage]; the
+// per-file blocks_hash chains (sha1_chain_kernel, another stream) consume a
+// stage as soon as all its waves have arrived.  rows*m must be a multiple
+// of 64 so that no wave straddles two stages.
 template <int TILE>
 __global__ void __launch_bounds__(kThreads)
-sha1_grid_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols,
-                 uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad) {
+sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
+                   uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
+                   uint32_t* __restrict__ stage_done) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nblocks = rows * cols;
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
   if (first >= nblocks) return;
+  const uint64_t per_stage = rows * m;
+  const uint64_t stage = first / per_stage;  // wave-uniform
   const uint64_t blk = first + lane;
   const bool valid = blk < nblocks;
-  const uint64_t b = valid ? blk : first;
-  const uint64_t row = b / cols, col = b - row * cols;
+  const uint64_t w = (valid ? blk : first) - stage * per_stage;
+  const uint64_t row = w / m, col = stage * m + (w - (w / m) * m);
   const uint64_t off = row * in_stride + col * bs;
-  const uint64_t last = (first + 64 <= nblocks) ? first + 63 : nblocks - 1;
-  const uint64_t r0 = first / cols, r1 = last / cols;
+  // wave span from the first and last block (same stage, rows ascending)
+  const uint64_t w0 = first - stage * per_stage;
+  const uint64_t wl = (first + 64 <= nblocks ? first + 63 : nblocks - 1) - stage * per_stage;
   WaveGeo geo;
-  geo.base = r0 * in_stride + (first - r0 * cols) * bs;
-  geo.span = r1 * in_stride + (last - r1 * cols) * bs + bs - geo.base;
+  geo.base = (w0 / m) * in_stride + (stage * m + w0 % m) * bs;
+  geo.span = (wl / m) * in_stride + (stage * m + wl % m) * bs + bs - geo.base;
   geo.min_size = bs;
   geo.max_size = bs;
   geo.max_nch = n_chunks(bs);
@@ -310,58 +318,84 @@ sha1_grid_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, u
   Sha1 st;
   hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
   if (valid) st.store(digests + (row * out_stride + col) * 20);
+  // Publish (MI355X guide, Guideline 16 counter form): drain the stores,
+  // agent-scope release (writes back this XCD's L2), drain again (hipcc may
+  // drop the fence's own wait), then one relaxed agent-scope add.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(stage_done + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One lane per file: advance the file's blocks_hash SHA-1 (src/index.rs:
-// 661-682) over bytes [lo, hi) of its digest run (hi - lo a multiple of 64),
-// keeping the chaining state in `state` (5 words per file) between stages;
-// `last` also hashes the rest of the run plus the padding and writes the
-// 20-byte blocks_hash.  The next chunk's loads are issued before the current
-// compression, since each chain is latency bound (one lane, one wave).
+// One lane per file: the file's blocks_hash (src/index.rs:661-682) = SHA-1
+// over its run of run_len digest bytes.  For each of S stages the wave waits
+// until stage_done[k] == waves_per_stage (bounded poll by one lane, then an
+// agent-scope acquire), then hashes that stage's slice [k*mb, (k+1)*mb) of
+// every file's run (mb a multiple of 64); the last stage adds the padding and
+// stores the 20-byte result.  A poll that times out (never expected: the
+// producer is already running or finished) stores an all-zero hash and sets
+// *timeout.  The next chunk's loads are issued before each compression,
+// since a chain is latency bound (one lane, one wave per CU).
 __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
-                  uint32_t lo, uint32_t hi, uint32_t* __restrict__ state, uint8_t* __restrict__ out, int first,
-                  int last) {
+                  uint32_t S, uint32_t mb, const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
+                  uint8_t* __restrict__ out, uint32_t* __restrict__ timeout) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  if (f >= nfiles) return;
+  const bool valid = f < nfiles;
   Sha1 st;
-  if (first) st.init();
-  else {
-    st.h0 = state[5 * f]; st.h1 = state[5 * f + 1]; st.h2 = state[5 * f + 2];
-    st.h3 = state[5 * f + 3]; st.h4 = state[5 * f + 4];
-  }
-  const uint8_t* p = runs + (uint64_t)f * run_stride;
+  st.init();
+  const uint8_t* p = runs + (uint64_t)(valid ? f : 0) * run_stride;
   const uint4* q = reinterpret_cast<const uint4*>(p);
-  uint32_t c = lo;
-  if (c + 64 <= hi) {
-    uint4 cur[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cur[j] = q[c / 16 + j];
-    for (; c + 64 <= hi; c += 64) {
-      uint4 nxt[4];
-      const bool more = c + 128 <= hi;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nxt[j] = more ? q[(c + 64) / 16 + j] : cur[j];
-      uint32_t w[16];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w[4 * j] = bswap32(cur[j].x); w[4 * j + 1] = bswap32(cur[j].y);
-        w[4 * j + 2] = bswap32(cur[j].z); w[4 * j + 3] = bswap32(cur[j].w);
+  bool ok = true;
+  for (uint32_t k = 0; k < S && ok; ++k) {
+    if (stage_done) {
+      // ONE lane polls ONE word (relaxed, agent scope), with s_sleep.
+      uint32_t seen = 0;
+      if (threadIdx.x == 0) {
+        for (uint32_t spins = 0;; ++spins) {
+          seen = __hip_atomic_load(stage_done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (seen >= waves_per_stage || spins > (1u << 24)) break;
+          __builtin_amdgcn_s_sleep(8);
+        }
       }
-      st.compress(w);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      seen = __builtin_amdgcn_readfirstlane(seen);
+      if (seen < waves_per_stage) {
+        ok = false;
+        if (threadIdx.x == 0) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!valid) continue;
+    const uint32_t lo = k * mb, hi = (k + 1 == S) ? (run_len / 64) * 64 : lo + mb;
+    if (lo + 64 <= hi) {
+      // software pipeline: the next chunk's four 16-B loads are in flight
+      // during the current compression (named registers, not arrays, so the
+      // loop-carried values stay in VGPRs).
+      uint4 c0 = q[lo / 16], c1 = q[lo / 16 + 1], c2 = q[lo / 16 + 2], c3 = q[lo / 16 + 3];
+      for (uint32_t c = lo; c + 64 <= hi; c += 64) {
+        const uint32_t nx = (c + 128 <= hi) ? (c + 64) / 16 : c / 16;
+        const uint4 n0 = q[nx], n1 = q[nx + 1], n2 = q[nx + 2], n3 = q[nx + 3];
+        uint32_t w[16] = {bswap32(c0.x), bswap32(c0.y), bswap32(c0.z), bswap32(c0.w),
+                          bswap32(c1.x), bswap32(c1.y), bswap32(c1.z), bswap32(c1.w),
+                          bswap32(c2.x), bswap32(c2.y), bswap32(c2.z), bswap32(c2.w),
+                          bswap32(c3.x), bswap32(c3.y), bswap32(c3.z), bswap32(c3.w)};
+        st.compress(w);
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+      }
     }
   }
-  if (!last) {
-    state[5 * f] = st.h0; state[5 * f + 1] = st.h1; state[5 * f + 2] = st.h2;
-    state[5 * f + 3] = st.h3; state[5 * f + 4] = st.h4;
+  if (!valid) return;
+  if (!ok) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + (uint64_t)f * 20);
+    o[0] = o[1] = o[2] = o[3] = o[4] = 0;
     return;
   }
   const uint32_t nch = n_chunks(run_len);
-  for (uint32_t k = c / 64; k < nch; ++k) {
+  for (uint32_t c = run_len / 64; c < nch; ++c) {
     uint32_t w[16];
-    build_tail_chunk(w, p, run_len, k, nch);
+    build_tail_chunk(w, p, run_len, c, nch);
     st.compress(w);
   }
   st.store(out + (uint64_t)f * 20);

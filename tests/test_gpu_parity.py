@@ -214,3 +214,24 @@ def test_batch_staged_chains(gpu, nfiles, nbf):
     fhn = fh.cpu().numpy()
     for i in range(nfiles):
         assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
+
+
+def test_batch_staged_repeated_calls_no_stale_digests(gpu):
+    # the chains read digests written by other CUs/XCDs of a concurrently
+    # running kernel: call repeatedly into the SAME output buffers with
+    # different data and check every result (a missing release/acquire
+    # shows up as stale digests from the previous call)
+    nfiles, nbf, bs = 128, 512, 4096
+    n = nfiles * nbf * bs
+    t = torch.empty(n, dtype=torch.uint8, device=gpu)
+    dig = torch.empty((nfiles * nbf, 20), dtype=torch.uint8, device=gpu)
+    fh = torch.empty((nfiles, 20), dtype=torch.uint8, device=gpu)
+    files = [(i * nbf * bs, nbf * bs) for i in range(nfiles)]
+    for seed in (7001, 7002, 7003):
+        device.fill_splitmix(t, seed)
+        device.index_device_batch(t, files, bs, out=dig, hashes_out=fh)
+        want = oracle.index_fixed_mt(oracle.splitmix_bytes(n, seed), bs, 8)
+        assert np.array_equal(dig.cpu().numpy(), want), seed
+        fhn = fh.cpu().numpy()
+        for i in range(nfiles):
+            assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), (seed, i)
