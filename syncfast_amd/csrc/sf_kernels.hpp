@@ -340,6 +340,9 @@ __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
                   uint32_t S, uint32_t mb, const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
                   uint8_t* __restrict__ out, uint32_t* __restrict__ timeout) {
+  // Latency-bound chains share SIMDs with the block kernel's waves: issue
+  // them first (priority outranks age), they need few issue slots.
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
   const bool valid = f < nfiles;
   Sha1 st;
@@ -377,6 +380,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
       for (uint32_t c = lo; c + 64 <= hi; c += 64) {
         const uint32_t nx = (c + 128 <= hi) ? (c + 64) / 16 : c / 16;
         const uint4 n0 = q[nx], n1 = q[nx + 1], n2 = q[nx + 2], n3 = q[nx + 3];
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compression
         uint32_t w[16] = {bswap32(c0.x), bswap32(c0.y), bswap32(c0.z), bswap32(c0.w),
                           bswap32(c1.x), bswap32(c1.y), bswap32(c1.z), bswap32(c1.w),
                           bswap32(c2.x), bswap32(c2.y), bswap32(c2.z), bswap32(c2.w),
