@@ -12,7 +12,6 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <mutex>
 #include <vector>
 
 #include "../../include/syncfast_amd.h"
@@ -101,35 +100,13 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
   return hip_err(hipGetLastError());
 }
 
-// A second stream per device for the per-file blocks_hash chains of the
-// staged batch (created once, kept for the process lifetime).
-hipStream_t side_stream(int* rc) {
-  static std::mutex mu;
-  static hipStream_t streams[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { *rc = SF_ENODEV; return nullptr; }
-  std::lock_guard<std::mutex> g(mu);
-  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess) {
-    *rc = SF_ENODEV;
-    return nullptr;
-  }
-  *rc = SF_OK;
-  return streams[dev];
-}
-
-// Many equal-size, block-aligned files back to back.  ONE launch hashes the
-// blocks in S column stages (stage k = blocks [k*m, (k+1)*m) of every file,
-// stage-major) and publishes per-stage arrival counters; the per-file
-// blocks_hash chains run concurrently on the side stream and consume each
-// stage as soon as it is complete.  Only the last stage's chains stay
-// exposed after the block hashing.  The side stream starts after the
-// counters are zeroed (event after the memset), and the caller's stream
-// resumes after the chains.
+// Many equal-size, block-aligned files back to back, with their per-file
+// blocks_hash.  Staged (S > 1): ONE launch of sha1_staged_kernel whose first
+// workgroups run the per-file chains while the others hash the blocks in S
+// column stages; only the last stage's chain work follows the last block.
+// Unstaged: the block kernel, then the stand-alone chain kernel.
 int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
                  uint8_t* fh, hipStream_t s) {
-  int rc = SF_OK;
-  hipStream_t side = side_stream(&rc);
-  if (rc) return rc;
   int S = 1;
   const char* se = getenv("SF_STAGES");  // A/B knob; default up to 16 stages
   const int smax = se ? std::max(1, atoi(se)) : 16;
@@ -138,33 +115,25 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
       S = cand;
       break;
     }
+  if (S == 1) {
+    int rc = launch_fixed(base, nbf * nfiles * (uint64_t)bs, bs, nbf * nfiles, dig, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3((unsigned)ceil_div(nfiles, 64)), dim3(64), 0, s, dig, nbf * 20,
+                       nfiles, (uint32_t)(nbf * 20), fh);
+    return hip_err(hipGetLastError());
+  }
   const uint64_t m = nbf / S;
-  const uint64_t per_stage = (uint64_t)nfiles * m;
-  const bool staged = S > 1;
   const sf::PadSchedule pad = pad_schedule(bs);
   uint32_t* words = nullptr;  // [0, 32): stage counters, [32]: timeout word; 16-B padded block
   const size_t wbytes = 48 * sizeof(uint32_t);
   SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  for (auto& e : ev) SF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  do {
-    if (hipEventRecord(ev[0], s) != hipSuccess) { rc = SF_ENODEV; break; }
-    const uint64_t nb = (uint64_t)nfiles * nbf;
-    hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid_for_blocks(nb)), dim3(sf::kThreads), 0, s, base, bs,
-                       (uint64_t)nfiles, nbf, m, flen, dig, nbf, pad, words);
-    if ((rc = hip_err(hipGetLastError()))) break;
-    // Unstaged: the chains simply follow the block kernel on the side stream.
-    if (hipStreamWaitEvent(side, ev[0], 0) != hipSuccess) { rc = SF_ENODEV; break; }
-    if (!staged && hipEventRecord(ev[1], s) == hipSuccess) (void)hipStreamWaitEvent(side, ev[1], 0);
-    hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3((unsigned)ceil_div(nfiles, 64)), dim3(64), 0, side, dig, nbf * 20,
-                       nfiles, (uint32_t)(nbf * 20), (uint32_t)S, (uint32_t)(m * 20),
-                       staged ? words : nullptr, (uint32_t)(per_stage / 64), fh, words + 32);
-    if ((rc = hip_err(hipGetLastError()))) break;
-    if (hipEventRecord(ev[1], side) != hipSuccess || hipStreamWaitEvent(s, ev[1], 0) != hipSuccess) rc = SF_ENODEV;
-  } while (0);
+  const unsigned chain_wgs = (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
+  const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
+  hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
+                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, words + 32);
+  int rc = hip_err(hipGetLastError());
   (void)hipFreeAsync(words, s);
-  for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
 }
 

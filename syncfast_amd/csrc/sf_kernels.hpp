@@ -275,86 +275,47 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   if (valid) st.store(digests + blk * 20);
 }
 
-// Many equal-size files, blocks hashed in column stages inside ONE launch.
-// `rows` files of `cols` full-size blocks; stage k = columns [k*m, (k+1)*m)
-// of every file, blocks numbered stage-major (stage, row, column), so the
-// dispatcher finishes stage k's waves roughly before stage k+1's.  Block
-// (row, col) reads data[row*in_stride + col*bs, +bs) and writes digest
-// out[row*out_stride + col].  After storing its 64 digests each wave
-// publishes (release, agent scope) one arrival on stage_done[stage]; the
-// per-file blocks_hash chains (sha1_chain_kernel, another stream) consume a
-// stage as soon as all its waves have arrived.  rows*m must be a multiple
-// of 64 so that no wave straddles two stages.
-template <int TILE>
-__global__ void __launch_bounds__(kThreads)
-sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
-                   uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
-                   uint32_t* __restrict__ stage_done) {
-  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nblocks = rows * cols;
-  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
-  if (first >= nblocks) return;
-  const uint64_t per_stage = rows * m;
-  const uint64_t stage = first / per_stage;  // wave-uniform
-  const uint64_t blk = first + lane;
-  const bool valid = blk < nblocks;
-  const uint64_t w = (valid ? blk : first) - stage * per_stage;
-  const uint64_t row = w / m, col = stage * m + (w - (w / m) * m);
-  const uint64_t off = row * in_stride + col * bs;
-  // wave span from the first and last block (same stage, rows ascending)
-  const uint64_t w0 = first - stage * per_stage;
-  const uint64_t wl = (first + 64 <= nblocks ? first + 63 : nblocks - 1) - stage * per_stage;
-  WaveGeo geo;
-  geo.base = (w0 / m) * in_stride + (stage * m + w0 % m) * bs;
-  geo.span = (wl / m) * in_stride + (stage * m + wl % m) * bs + bs - geo.base;
-  geo.min_size = bs;
-  geo.max_size = bs;
-  geo.max_nch = n_chunks(bs);
-  geo.lds_ok = ((bs & 15u) == 0) && ((in_stride & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
-               geo.span < 0xF0000000ull;
-  const uint32_t rel = (uint32_t)(off - geo.base);
-  Sha1 st;
-  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
-  if (valid) st.store(digests + (row * out_stride + col) * 20);
-  // Publish (MI355X guide, Guideline 16 counter form): drain the stores,
-  // agent-scope release (writes back this XCD's L2), drain again (hipcc may
-  // drop the fence's own wait), then one relaxed agent-scope add.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(stage_done + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Stream a 64-B-multiple byte range [lo, hi) of a lane's message through
+// SHA-1, the next chunk's loads issued before each compression (the load
+// has a whole compression to land; one register set keeps the VGPR count
+// under the block kernel's when fused with it).
+__device__ __forceinline__ void sha1_stream_range(Sha1& st, const uint4* __restrict__ q, uint32_t lo, uint32_t hi) {
+  if (lo + 64 > hi) return;
+  uint4 c0 = q[lo / 16], c1 = q[lo / 16 + 1], c2 = q[lo / 16 + 2], c3 = q[lo / 16 + 3];
+  for (uint32_t c = lo; c + 64 <= hi; c += 64) {
+    const uint32_t nx = (c + 128 <= hi) ? (c + 64) / 16 : c / 16;
+    const uint4 n0 = q[nx], n1 = q[nx + 1], n2 = q[nx + 2], n3 = q[nx + 3];
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t w[16] = {bswap32(c0.x), bswap32(c0.y), bswap32(c0.z), bswap32(c0.w),
+                      bswap32(c1.x), bswap32(c1.y), bswap32(c1.z), bswap32(c1.w),
+                      bswap32(c2.x), bswap32(c2.y), bswap32(c2.z), bswap32(c2.w),
+                      bswap32(c3.x), bswap32(c3.y), bswap32(c3.z), bswap32(c3.w)};
+    st.compress(w);
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
 }
 
 // One lane per file: the file's blocks_hash (src/index.rs:661-682) = SHA-1
-// over its run of run_len digest bytes.  For each of S stages the wave waits
-// until stage_done[k] == waves_per_stage (bounded poll by one lane, then an
-// agent-scope acquire), then hashes that stage's slice [k*mb, (k+1)*mb) of
-// every file's run (mb a multiple of 64); the last stage adds the padding and
-// stores the 20-byte result.  A poll that times out (never expected: the
-// producer is already running or finished) stores an all-zero hash and sets
-// *timeout.  The next chunk's loads are issued before each compression,
-// since a chain is latency bound (one lane, one wave per CU).
-__global__ void __launch_bounds__(64)
-sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
-                  uint32_t S, uint32_t mb, const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
-                  uint8_t* __restrict__ out, uint32_t* __restrict__ timeout) {
-  // Latency-bound chains share SIMDs with the block kernel's waves: issue
-  // them first (priority outranks age), they need few issue slots.
-  __builtin_amdgcn_s_setprio(3);
-  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  const bool valid = f < nfiles;
+// over its run of run_len digest bytes, consumed in S slices of mb bytes (a
+// multiple of 64).  With stage_done, slice k is read only after
+// stage_done[k] == waves_per_stage: ONE lane polls ONE word (relaxed, agent
+// scope, s_sleep, bounded), then an agent-scope acquire (MI355X guide,
+// Guideline 16).  A poll that gives up stores an all-zero hash and sets
+// *timeout (never expected: the producers never wait).
+__device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t f,
+                                           bool valid, uint32_t run_len, uint32_t S, uint32_t mb,
+                                           const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
+                                           uint8_t* __restrict__ out, uint32_t* __restrict__ timeout) {
+  const int lane = threadIdx.x & 63;
   Sha1 st;
   st.init();
   const uint8_t* p = runs + (uint64_t)(valid ? f : 0) * run_stride;
   const uint4* q = reinterpret_cast<const uint4*>(p);
   bool ok = true;
-  for (uint32_t k = 0; k < S && ok; ++k) {
+  for (uint32_t k = 0; k < S; ++k) {
     if (stage_done) {
-      // ONE lane polls ONE word (relaxed, agent scope), with s_sleep.
       uint32_t seen = 0;
-      if (threadIdx.x == 0) {
+      if (lane == 0) {
         for (uint32_t spins = 0;; ++spins) {
           seen = __hip_atomic_load(stage_done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (seen >= waves_per_stage || spins > (1u << 24)) break;
@@ -364,30 +325,15 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
       seen = __builtin_amdgcn_readfirstlane(seen);
       if (seen < waves_per_stage) {
         ok = false;
-        if (threadIdx.x == 0) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (!valid) continue;
-    const uint32_t lo = k * mb, hi = (k + 1 == S) ? (run_len / 64) * 64 : lo + mb;
-    if (lo + 64 <= hi) {
-      // software pipeline: the next chunk's four 16-B loads are in flight
-      // during the current compression (named registers, not arrays, so the
-      // loop-carried values stay in VGPRs).
-      uint4 c0 = q[lo / 16], c1 = q[lo / 16 + 1], c2 = q[lo / 16 + 2], c3 = q[lo / 16 + 3];
-      for (uint32_t c = lo; c + 64 <= hi; c += 64) {
-        const uint32_t nx = (c + 128 <= hi) ? (c + 64) / 16 : c / 16;
-        const uint4 n0 = q[nx], n1 = q[nx + 1], n2 = q[nx + 2], n3 = q[nx + 3];
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the compression
-        uint32_t w[16] = {bswap32(c0.x), bswap32(c0.y), bswap32(c0.z), bswap32(c0.w),
-                          bswap32(c1.x), bswap32(c1.y), bswap32(c1.z), bswap32(c1.w),
-                          bswap32(c2.x), bswap32(c2.y), bswap32(c2.z), bswap32(c2.w),
-                          bswap32(c3.x), bswap32(c3.y), bswap32(c3.z), bswap32(c3.w)};
-        st.compress(w);
-        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-      }
+    if (valid) {
+      const uint32_t lo = k * mb, hi = (k + 1 == S) ? (run_len / 64) * 64 : lo + mb;
+      sha1_stream_range(st, q, lo, hi);
     }
   }
   if (!valid) return;
@@ -403,6 +349,72 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
     st.compress(w);
   }
   st.store(out + (uint64_t)f * 20);
+}
+
+// Stand-alone chains (no stages): one lane per file over its whole run.
+__global__ void __launch_bounds__(64)
+sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
+                  uint8_t* __restrict__ out) {
+  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr);
+}
+
+// Many equal-size files in ONE launch with their blocks_hash chains.
+// `rows` files of `cols` full-size blocks.  Workgroups [0, chain_wgs) are
+// chain workgroups: each wave owns 64 files and runs chain_wave over S
+// stages.  The others hash blocks: stage k = columns [k*m, (k+1)*m) of every
+// file, numbered stage-major (stage, row, column) so the dispatcher finishes
+// stage k roughly before stage k+1; block (row, col) reads
+// data[row*in_stride + col*bs, +bs) and writes out[row*out_stride + col].
+// After storing its 64 digests each block wave publishes one arrival on
+// stage_done[stage] (drain, agent release, drain, relaxed agent add).
+// Deadlock-free by construction: only chain waves wait, and only on block
+// waves, which never wait; the bounded poll is a backstop.
+// rows*m must be a multiple of 64 (no wave straddles two stages).
+template <int TILE>
+__global__ void __launch_bounds__(kThreads, 4)  // keep 4 waves/SIMD (<= 128 VGPRs) with both roles
+sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
+                   uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
+                   uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
+                   uint32_t* __restrict__ timeout) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t per_stage = rows * m;
+  if (blockIdx.x < chain_wgs) {
+    __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
+    const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + lane;
+    chain_wave(digests, out_stride * 20, f, f < rows, (uint32_t)(cols * 20), (uint32_t)(cols / m),
+               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, timeout);
+    return;
+  }
+  const uint64_t nblocks = rows * cols;
+  const uint64_t first = ((uint64_t)(blockIdx.x - chain_wgs) * kWavesPerWG + wid) * 64;
+  if (first >= nblocks) return;
+  const uint64_t stage = first / per_stage;  // wave-uniform
+  const uint64_t blk = first + lane;
+  const bool valid = blk < nblocks;
+  const uint64_t w = (valid ? blk : first) - stage * per_stage;
+  const uint64_t row = w / m, col = stage * m + (w - (w / m) * m);
+  const uint64_t off = row * in_stride + col * bs;
+  const uint64_t w0 = first - stage * per_stage;
+  const uint64_t wl = (first + 64 <= nblocks ? first + 63 : nblocks - 1) - stage * per_stage;
+  WaveGeo geo;
+  geo.base = (w0 / m) * in_stride + (stage * m + w0 % m) * bs;
+  geo.span = (wl / m) * in_stride + (stage * m + wl % m) * bs + bs - geo.base;
+  geo.min_size = bs;
+  geo.max_size = bs;
+  geo.max_nch = n_chunks(bs);
+  geo.lds_ok = ((bs & 15u) == 0) && ((in_stride & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
+               geo.span < 0xF0000000ull;
+  const uint32_t rel = (uint32_t)(off - geo.base);
+  Sha1 st;
+  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
+  if (valid) st.store(digests + (row * out_stride + col) * 20);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(stage_done + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
