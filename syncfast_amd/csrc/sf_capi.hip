@@ -128,10 +128,14 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   const size_t wbytes = 48 * sizeof(uint32_t);
   SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
-  const unsigned chain_wgs = (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
+  // Experiment knob SF_STAGED_EXP: 1 = no chain workgroups (publish only),
+  // 2 = no chains and no publish (block hashing in stage order only).
+  const char* xe = getenv("SF_STAGED_EXP");
+  const int exp = xe ? atoi(xe) : 0;
+  const unsigned chain_wgs = exp ? 0u : (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
   const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
-                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, words + 32);
+                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, exp == 2 ? nullptr : fh, words + 32);
   int rc = hip_err(hipGetLastError());
   (void)hipFreeAsync(words, s);
   return rc;

@@ -411,6 +411,7 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
   Sha1 st;
   hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
   if (valid) st.store(digests + (row * out_stride + col) * 20);
+  if (chain_wgs == 0 && file_hashes == nullptr) return;  // experiment: blocks only, no publish
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
