@@ -80,6 +80,17 @@ struct Sha1 {
     }
     h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
   }
+  // Same bytes, stored write-through (sc1: global_store_dword ... sc1) so a
+  // consumer on another XCD can read them after a drain + flag, without an
+  // agent-scope release fence on this side.
+  __device__ __forceinline__ void store_writethrough(uint8_t* out20) const {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out20);
+    __hip_atomic_store(o + 0, bswap32(h0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 1, bswap32(h1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 2, bswap32(h2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 3, bswap32(h3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 4, bswap32(h4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // Digest bytes in sha1.digest().bytes() order (big-endian), as 5 words
   // ready for a little-endian store.
   __device__ __forceinline__ void store(uint8_t* out20) const {
