@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     p.add_argument("--shard-gib", type=float, default=None, help="override bytes per rank (GiB)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    p.add_argument("--ramp-s", type=float, default=0.5,
+                   help="setup: keep the kernel busy this long before the warmup steps (the chip takes "
+                        "~6 launches to ramp its clock from ~1.6 GHz; see DESIGN.md section 4)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
@@ -162,6 +165,11 @@ def main():
                 last_table[0] = finish()
                 pending[b] = None
 
+    # Setup (not a step): clock ramp, untimed, no gather.
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < a.ramp_s:
+        device.index_device(data, bs, out=digs[0], stream=stream)
+        torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i, False)
     drain()
