@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "../../include/syncfast_amd.h"
@@ -464,13 +465,28 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   if (n_out) *n_out = nb;
   if (nb > cap) { close(fd); return SF_ENOSPC; }
   if (nb && !out) { close(fd); return SF_EINVAL; }
+  // Each stage is read by several threads in parallel (one pread stream per
+  // slice): one thread copies from the page cache at ~16 GB/s, below PCIe.
+  const unsigned nthreads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   rc = index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
-    uint64_t got = 0;
-    while (got < n) {
-      const ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
-      if (r <= 0) return SF_EIO;
-      got += (uint64_t)r;
-    }
+    auto read_slice = [&](uint64_t a, uint64_t b) {
+      uint64_t got = a;
+      while (got < b) {
+        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(off + got));
+        if (r <= 0) return SF_EIO;
+        got += (uint64_t)r;
+      }
+      return SF_OK;
+    };
+    const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
+    std::vector<std::thread> pool;
+    std::vector<int> rcs(nthreads, SF_OK);
+    for (unsigned t = 1; t < nthreads && t * slice < n; t++)
+      pool.emplace_back([&, t] { rcs[t] = read_slice(t * slice, std::min(n, (t + 1) * slice)); });
+    rcs[0] = read_slice(0, std::min(n, slice));
+    for (auto& th : pool) th.join();
+    for (int r : rcs)
+      if (r) return r;
     return SF_OK;
   });
   close(fd);
