@@ -103,6 +103,16 @@ int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
                           uint64_t *n_blocks, void *stream);
 
+/* The signature table as the reference's wire messages, on the device:
+ * n_blocks FILE_BLOCK messages, "FILE_BLOCK\n" + 20 digest bytes + "\n" +
+ * decimal block size + "\n" (write_message, src/sync/ssh/proto.rs:162-166),
+ * what FsSource sends per block after FILE_START (src/sync/fs.rs:217-233).
+ * Fixed tiling of a file_len-byte file.  *n_out = bytes written (the need,
+ * with SF_ENOSPC, when cap is too small). */
+int sf_wire_file_blocks_device(const void *d_digests, uint64_t n_blocks, uint32_t block_size,
+                               uint64_t file_len, void *d_out, uint64_t cap, uint64_t *n_out,
+                               void *stream);
+
 /* Deterministic synthetic input (bench / tests): bytes [start, start+len)
  * of the splitmix64 stream with this seed. */
 int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t start, void *stream);

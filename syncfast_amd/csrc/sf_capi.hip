@@ -375,6 +375,26 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   return SF_OK;
 }
 
+int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len,
+                               void* d_out, uint64_t cap, uint64_t* n_out, void* stream) {
+  if (block_size == 0 || block_size > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
+  const uint64_t nb = file_len ? ceil_div(file_len, block_size) : 0;
+  if (nb != n_blocks) return SF_EINVAL;
+  uint64_t db = 1;
+  for (uint64_t v = block_size; v >= 10; v /= 10) db++;
+  const uint32_t last = nb ? (uint32_t)(file_len - (nb - 1) * block_size) : 0;
+  uint64_t dl = 1;
+  for (uint64_t v = last; v >= 10; v /= 10) dl++;
+  const uint64_t bytes = nb ? (nb - 1) * (33 + db) + (33 + dl) : 0;
+  if (n_out) *n_out = bytes;
+  if (bytes > cap) return SF_ENOSPC;
+  if (!nb) return SF_OK;
+  if (!d_digests || !d_out) return SF_EINVAL;
+  hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint8_t*>(d_digests), nb, block_size, last, static_cast<uint8_t*>(d_out));
+  return hip_err(hipGetLastError());
+}
+
 int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t start, void* stream) {
   if (len == 0) return SF_OK;
   if (!d_out) return SF_EINVAL;

@@ -477,6 +477,38 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   }
 }
 
+// Wire emission of the signature table as the reference's FILE_BLOCK
+// messages (src/sync/ssh/proto.rs:162-166): "FILE_BLOCK\n" + 20 raw digest
+// bytes + "\n" + decimal size + "\n".  Fixed tiling: every block is
+// block_size bytes except the last (last_size), so message i starts at
+// i * (33 + digits(block_size)).  One thread per message, byte stores.
+__device__ __forceinline__ uint32_t dec_digits(uint64_t v) {
+  uint32_t d = 1;
+  while (v >= 10) { v /= 10; ++d; }
+  return d;
+}
+
+__global__ void __launch_bounds__(256)
+wire_file_blocks_kernel(const uint8_t* __restrict__ digests, uint64_t n, uint32_t block_size, uint32_t last_size,
+                        uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t db = dec_digits(block_size);
+  const uint64_t msg = 33 + db;  // 11 + 20 + 1 + digits + 1
+  uint8_t* o = out + i * msg;
+  const char tag[11] = {'F', 'I', 'L', 'E', '_', 'B', 'L', 'O', 'C', 'K', '\n'};
+#pragma unroll
+  for (int k = 0; k < 11; ++k) o[k] = (uint8_t)tag[k];
+  const uint8_t* d = digests + i * 20;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) o[11 + k] = d[k];
+  o[31] = '\n';
+  uint32_t v = (i + 1 == n) ? last_size : block_size;
+  const uint32_t nd = dec_digits(v);
+  for (int k = (int)nd - 1; k >= 0; --k) { o[32 + k] = (uint8_t)('0' + v % 10); v /= 10; }
+  o[32 + nd] = '\n';
+}
+
 // splitmix64 byte stream: word i = mix(seed + (i+1)*GAMMA),
 // little-endian; writes bytes [start, start+len) of the stream.
 __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
