@@ -124,14 +124,15 @@ def test_reference_index_kat(gpu, tmp_path):
 
 
 @pytest.mark.gpu
-def test_index_path_fixed_blocks(gpu, tmp_path):
+@pytest.mark.parametrize("batch_bytes", [0, 1 << 30, 50_000])
+def test_index_path_fixed_blocks(gpu, tmp_path, batch_bytes):
     root = tmp_path / "tree"
     (root / "sub").mkdir(parents=True)
     files = {"a.bin": 100_000, "sub/b.bin": 4096 * 3, "sub/empty": 0, "c": 1}
     for i, (n, ln) in enumerate(files.items()):
         (root / n).write_bytes(oracle.splitmix_bytes(ln, 1000 + i).tobytes())
     idx = Index.open(root / ".syncfast.idx", chunker=FixedChunker(4096))
-    idx.index_path(root)
+    idx.index_path(root, batch_bytes=batch_bytes)
     idx.remove_missing_files(root)
     idx.commit()
     names = {str(f[1]) for f in idx.list_files()}
@@ -143,10 +144,11 @@ def test_index_path_fixed_blocks(gpu, tmp_path):
         got = idx.list_file_blocks(fid)
         assert [(g[0].bytes, g[1], g[2]) for g in got] == [(bytes(w), int(o), int(s)) for w, o, s in zip(want, offs, sizes)]
         assert bh.bytes == oracle.blocks_hash(want)
+        assert idx.compute_blocks_hash(fid) == bh  # device blocks_hash == reference recomputation
     # unchanged mtimes -> nothing re-indexed; a touched file is re-indexed
     before = idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0]
     os.utime(root / "c", ns=(1, 1))
-    idx.index_path(root)
+    idx.index_path(root, batch_bytes=batch_bytes)
     idx.commit()
     assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
     os.remove(root / "sub" / "b.bin")
