@@ -1,5 +1,9 @@
 """Interleaved A/B of kernel variants in ONE process (cdna guide rule 24).
 
+Needs a tuning build of the library (the variants are compiled only with
+-DSF_TUNING):  make -C syncfast_amd/csrc variant NAME=tuning EXTRA=-DSF_TUNING
+and SF_LIB=syncfast_amd/csrc/build/variants/libsf_tuning.so.
+
 Variants are selected per call through env knobs read by the C-ABI
 (SF_VARIANT: 0 shipped = <128,1>, 1 = <128,5>, 2 = <64,6>, 3 = <64,8>, 4 = <64,1>).  Reports median / min ms per launch over rounds and checks that
 every variant produces identical digests."""

@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsyncfast_amd.so")
+# SF_LIB overrides the library path (tuning builds, scripts/tune*.py only).
+LIB_PATH = os.environ.get("SF_LIB") or os.path.join(_HERE, "lib", "libsyncfast_amd.so")
 
 SF_OK = 0
 SF_EIO = -5

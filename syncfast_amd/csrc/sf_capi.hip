@@ -24,13 +24,12 @@ namespace {
 
 constexpr int kTile = 128;  // bytes of each block staged per LDS step
 
-// Tuning knob for experiments (interleaved A/B in one process): SF_VARIANT
-// selects a (tile, waves-per-SIMD) build of the fixed kernel; 0 = shipped.
-// Read on every call.
+#ifdef SF_TUNING
 inline int variant_choice() {
   const char* e = getenv("SF_VARIANT");
   return e ? atoi(e) : 0;
 }
+#endif
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -81,6 +80,9 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   const sf::PadSchedule pad = pad_schedule(bs);
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
   uint8_t* o = static_cast<uint8_t*>(d_digests);
+#ifdef SF_TUNING
+  // Tuning builds only (make variant EXTRA=-DSF_TUNING): SF_VARIANT selects a
+  // (tile, waves-per-SIMD) instantiation for interleaved A/B in one process.
   switch (variant_choice()) {
     case 1: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 5>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
@@ -88,6 +90,9 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
     case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
   }
+#else
+  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
+#endif
   return hip_err(hipGetLastError());
 }
 
@@ -129,10 +134,14 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   const size_t wbytes = 48 * sizeof(uint32_t);
   SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
-  // Experiment knob SF_STAGED_EXP: 1 = no chain workgroups (publish only),
-  // 2 = no chains and no publish (block hashing in stage order only).
+#ifdef SF_TUNING
+  // SF_STAGED_EXP: 1 = no chain workgroups (publish only), 2 = no chains and
+  // no publish (block hashing in stage order only) -- cost breakdown only.
   const char* xe = getenv("SF_STAGED_EXP");
   const int exp = xe ? atoi(xe) : 0;
+#else
+  const int exp = 0;
+#endif
   const unsigned chain_wgs = exp ? 0u : (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
   const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
