@@ -37,7 +37,7 @@ def main():
     # clock ramp
     for _ in range(40):
         Ls[0](data.data_ptr(), size, bs, outs[0].data_ptr(), n, ctypes.byref(nb), s.cuda_stream)
-    for r in range(6):
+    for r in range(int(os.environ.get("TUNE_ROUNDS", "6"))):
         for i, f in enumerate(Ls):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)

@@ -138,9 +138,12 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
   const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
   __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
+#ifndef SF_LOAD_AUX
+#define SF_LOAD_AUX 0  // cache policy bits of the DMA loads (2 = nt), A/B via make variant
+#endif
 #pragma unroll
   for (int j = 0; j < TILE / 16; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
 }
 
 // Hash the block (off, size) owned by this lane; all 64 lanes of the wave
