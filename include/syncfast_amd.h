@@ -96,8 +96,8 @@ int sf_index_device_blocks(const void *d_data, uint64_t len, const uint64_t *d_o
  * file, to d_digests (cap_blocks rows) and, if d_file_hashes != NULL, each
  * file's blocks_hash (20 B per file, src/index.rs:661-682) computed on the
  * device.  first_block (host, n_files+1 entries, may be NULL) receives the
- * index of each file's first digest row; *n_blocks the total.  Synchronous
- * w.r.t. the host for its small block-table upload only. */
+ * index of each file's first digest row; *n_blocks the total.  Asynchronous
+ * on `stream` (ragged batches upload a small block table, stream-ordered). */
 int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *files,
                           uint32_t n_files, uint32_t block_size, void *d_digests,
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,

@@ -88,6 +88,9 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
     case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     case 3: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 8>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 5: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 4>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 6: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 2>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 7: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 3>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
   }
 #else
@@ -353,35 +356,39 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
       h_fsz[f] = (uint32_t)(nbf * 20);
     }
   }
-  DevBuf ws;
-  if (tbl_bytes + fh_bytes) {
-    SF_HIP(hipMalloc(&ws.p, tbl_bytes + fh_bytes));
-    SF_HIP(hipMemcpy(ws.p, host_ws.data(), tbl_bytes + fh_bytes, hipMemcpyHostToDevice));
+  // Stream-ordered workspace: allocated, filled, used and freed on `s`, so
+  // the call stays asynchronous.  (hipMemcpyAsync from pageable memory
+  // returns once the bytes are staged, so host_ws may go out of scope.)
+  uint8_t* dws = nullptr;
+  const size_t ws_bytes = tbl_bytes + fh_bytes;
+  if (ws_bytes) {
+    SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&dws), ws_bytes, s));
+    SF_HIP(hipMemcpyAsync(dws, host_ws.data(), ws_bytes, hipMemcpyHostToDevice, s));
   }
-  uint8_t* dws = static_cast<uint8_t*>(ws.p);
-  if (total) {
-    if (contiguous_aligned) {
-      const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
-      rc = launch_fixed(base, fb[n_files] * (uint64_t)block_size, block_size, total, d_digests, s);
-    } else {
-      rc = launch_table(d_data, len, reinterpret_cast<const uint64_t*>(dws),
-                        reinterpret_cast<const uint32_t*>(dws + total * sizeof(uint64_t)), total, d_digests,
-                        nullptr, s);
+  do {
+    if (total) {
+      if (contiguous_aligned) {
+        const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
+        rc = launch_fixed(base, fb[n_files] * (uint64_t)block_size, block_size, total, d_digests, s);
+      } else {
+        rc = launch_table(d_data, len, reinterpret_cast<const uint64_t*>(dws),
+                          reinterpret_cast<const uint32_t*>(dws + total * sizeof(uint64_t)), total, d_digests,
+                          nullptr, s);
+      }
+      if (rc) break;
     }
-    if (rc) return rc;
-  }
-  if (need_fh) {
-    // blocks_hash of every file at once: one lane per file hashes its own
-    // run of 20-byte digests (a file with no blocks hashes the empty string).
-    const uint8_t* dg = total ? static_cast<const uint8_t*>(d_digests) : static_cast<const uint8_t*>(d_file_hashes);
-    rc = launch_table(dg, total * 20, reinterpret_cast<const uint64_t*>(dws + tbl_bytes),
-                      reinterpret_cast<const uint32_t*>(dws + tbl_bytes + n_files * sizeof(uint64_t)), n_files,
-                      d_file_hashes, nullptr, s);
-    if (rc) return rc;
-  }
-  // The workspace is freed on return: keep the stream ordered before that.
-  SF_HIP(hipStreamSynchronize(s));
-  return SF_OK;
+    if (need_fh) {
+      // blocks_hash of every file at once: one lane per file hashes its own
+      // run of 20-byte digests (a file with no blocks hashes the empty string).
+      const uint8_t* dg =
+          total ? static_cast<const uint8_t*>(d_digests) : static_cast<const uint8_t*>(d_file_hashes);
+      rc = launch_table(dg, total * 20, reinterpret_cast<const uint64_t*>(dws + tbl_bytes),
+                        reinterpret_cast<const uint32_t*>(dws + tbl_bytes + n_files * sizeof(uint64_t)), n_files,
+                        d_file_hashes, nullptr, s);
+    }
+  } while (0);
+  if (dws) (void)hipFreeAsync(dws, s);
+  return rc;
 }
 
 int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len,
