@@ -374,8 +374,11 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 // Deadlock-free by construction: only chain waves wait, and only on block
 // waves, which never wait; the bounded poll is a backstop.
 // rows*m must be a multiple of 64 (no wave straddles two stages).
+#ifndef SF_STAGED_WPE
+#define SF_STAGED_WPE 4  // min waves/SIMD of the staged kernel (A/B: make variant EXTRA=-DSF_STAGED_WPE=1)
+#endif
 template <int TILE>
-__global__ void __launch_bounds__(kThreads, 4)  // keep 4 waves/SIMD (<= 128 VGPRs) with both roles
+__global__ void __launch_bounds__(kThreads, SF_STAGED_WPE)
 sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
                    uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
                    uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
