@@ -34,6 +34,17 @@ def test_config2_8gib_4k_every_digest(gpu):
     bad = np.nonzero((dig != want).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} digests differ, first at block {bad[:5]}"
     assert host.blocks_hash(dig) == oracle.blocks_hash(want)
+    # explicit blocks scattered over the whole 8 GiB: most waves span more
+    # than 4 GiB and take the per-lane path; some are 16-B aligned
+    rng = np.random.default_rng(8)
+    m = 3000
+    sizes = rng.integers(0, 70_000, m)
+    offs = np.array([int(rng.integers(0, n - s)) for s in sizes], np.int64)
+    offs[::3] = offs[::3] // 16 * 16
+    data_t = torch.from_numpy(host_bytes).to(gpu)
+    dt = device.index_device_blocks(data_t, torch.from_numpy(offs).to(gpu),
+                                    torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
+    assert np.array_equal(dt, oracle.index_blocks(host_bytes, offs, sizes))
 
 
 def test_config5_32gib_64k_properties(gpu):

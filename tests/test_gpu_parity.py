@@ -60,7 +60,7 @@ def test_ragged_golden_on_device(gpu, golden):
         assert hexes(d) == case["digests"]
 
 
-@pytest.mark.parametrize("bs", [1, 16, 64, 100, 1000, 4095, 4096, 4097, 8192, 65536, 1 << 20])
+@pytest.mark.parametrize("bs", [1, 16, 64, 80, 100, 1000, 4080, 4095, 4096, 4097, 4112, 8192, 65536, 1 << 20])
 def test_fixed_random_lengths(gpu, bs):
     rng = np.random.default_rng(bs)
     for _ in range(3):
@@ -235,3 +235,15 @@ def test_batch_staged_repeated_calls_no_stale_digests(gpu):
         fhn = fh.cpu().numpy()
         for i in range(nfiles):
             assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), (seed, i)
+
+
+def test_max_block_size(gpu):
+    # SF_MAX_BLOCK_SIZE = 32 MiB: 64 such blocks span 2 GiB (still one LDS span)
+    bs = 32 << 20
+    n = 2 * bs + 12345
+    data = oracle.splitmix_bytes(n, 96)
+    d = device.index_device(to_dev(data.tobytes(), gpu), bs)
+    _, _, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(d.cpu().numpy(), want)
+    with pytest.raises(SfError):
+        device.index_device(to_dev(b"x" * 100, gpu), bs + 1)
