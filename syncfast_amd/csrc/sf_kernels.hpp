@@ -138,6 +138,9 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
   const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
   __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
+#ifndef SF_PIPE
+#define SF_PIPE 0  // 1: split LDS-read wait / mid-step DMA issue (A/B variant)
+#endif
 #ifndef SF_LOAD_AUX
 #define SF_LOAD_AUX 2  // nt: the input is streamed once (+1.4% in A/B, profiles/r01/tune_sched_nt.log)
 #endif
@@ -189,8 +192,14 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < PIECES; ++k) raw[k] = my[k ^ g];
+#if SF_PIPE
+      // Variant: only chunk 0's reads are waited for here (hipcc inserts the
+      // counted lgkmcnt before their first use); the rest land during
+      // chunk 0's compression, and the next DMA is issued after it.
+#else
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (t + 1 < nsteps) issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+#endif
 #else
       // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_NOLOAD):
       // same VALU work on register data, no loads -- isolates compute cost.
@@ -199,6 +208,16 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 #endif
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
+#if SF_PIPE && !defined(SF_EXPERIMENT_NOLOAD)
+        if (ch == 1) {
+          __builtin_amdgcn_sched_barrier(0);  // keep chunk 1's uses (and their waits) after chunk 0
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: reads done before the DMA rewrites the tile
+          // unconditional (no branch in the loop body): past the last step
+          // the resource has num_records 0, every lane reads zeros, nobody
+          // reads the tile again.
+          issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+        }
+#endif
         uint32_t w[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
