@@ -91,6 +91,14 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
     case 5: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 4>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     case 6: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 2>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
     case 7: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 3>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 8:
+      if (bs % 64 == 0 && (reinterpret_cast<uintptr_t>(d) & 15u) == 0) {
+        hipLaunchKernelGGL(sf::sha1_fixed2_kernel, dim3((unsigned)ceil_div(ceil_div(nblocks, 128), sf::kWavesPerWG)),
+                           dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
+        break;
+      }
+      hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
+      break;
     default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
   }
 #else

@@ -381,6 +381,89 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
   chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr);
 }
 
+#ifdef SF_TUNING
+// Tuning variant: TWO blocks per lane (wave = 128 consecutive blocks; lane l
+// owns blocks l and 64 + l), 64-B LDS steps (8 KiB tile per wave), the two
+// compressions round-interleaved.  Fixed tiling, bs % 64 == 0, 16-B aligned
+// data; anything else goes through the one-block kernel.
+__global__ void __launch_bounds__(kThreads)
+sha1_fixed2_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
+                   uint8_t* __restrict__ digests, const PadSchedule pad) {
+  constexpr int TILE = 64, PIECES = 4;
+  __shared__ uint4 smem[kWavesPerWG * 128 * PIECES];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 128;
+  if (first >= nblocks) return;
+  uint4* tile = smem + wid * 128 * PIECES;
+  const uint64_t blkA = first + lane, blkB = first + 64 + lane;
+  const bool vA = blkA < nblocks, vB = blkB < nblocks;
+  const uint32_t sA = vA ? (uint32_t)(len - blkA * bs < bs ? len - blkA * bs : bs) : 0u;
+  const uint32_t sB = vB ? (uint32_t)(len - blkB * bs < bs ? len - blkB * bs : bs) : 0u;
+  const uint64_t base = first * bs;
+  const uint64_t nvalid = nblocks - first < 128 ? nblocks - first : 128;
+  const uint64_t span = len - base < nvalid * (uint64_t)bs ? len - base : nvalid * (uint64_t)bs;
+  const uint64_t lastb = first + nvalid - 1;
+  const uint32_t last_size = (uint32_t)(len - lastb * bs < bs ? len - lastb * bs : bs);
+  const uint32_t min_size = last_size < bs ? last_size : bs;
+  Sha1 A, B;
+  A.init();
+  B.init();
+  const uint32_t nsteps = min_size / 64u;
+  uint32_t voff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int b = j * 16 + lane / 4;
+    const int k = (lane % 4) ^ ((b >> 2) & 3);
+    voff[j] = (uint32_t)b * bs + (uint32_t)k * 16u;
+  }
+  const int g = (lane >> 2) & 3;
+  const uint4* myA = tile + lane * PIECES;
+  const uint4* myB = tile + (64 + lane) * PIECES;
+  const uint8_t* span_ptr = data + base;
+  auto issue = [&](uint32_t step) {
+    const uint64_t toff = (uint64_t)step * TILE;
+    const uint64_t left = span > toff ? span - toff : 0;
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane(left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left);
+    const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
+  };
+  if (nsteps > 0) issue(0);
+  for (uint32_t t = 0; t < nsteps; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint4 ra[4], rb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { ra[k] = myA[k ^ g]; rb[k] = myB[k ^ g]; }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nsteps) issue(t + 1);
+    uint32_t wa[16], wb[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wa[4 * q] = bswap32(ra[q].x); wa[4 * q + 1] = bswap32(ra[q].y); wa[4 * q + 2] = bswap32(ra[q].z); wa[4 * q + 3] = bswap32(ra[q].w);
+      wb[4 * q] = bswap32(rb[q].x); wb[4 * q + 1] = bswap32(rb[q].y); wb[4 * q + 2] = bswap32(rb[q].z); wb[4 * q + 3] = bswap32(rb[q].w);
+    }
+    Sha1::compress2(A, wa, B, wb);
+  }
+  if (pad.bytes == min_size && min_size == bs) {
+    A.compress_uniform(pad.kw);
+    B.compress_uniform(pad.kw);
+  } else {
+    const uint32_t ncA = n_chunks(sA), ncB = n_chunks(sB);
+    const uint32_t mx = n_chunks(bs);
+    for (uint32_t c = nsteps; c < mx; ++c) {
+      if (vA && c < ncA) { uint32_t w[16]; build_tail_chunk(w, data + blkA * bs, sA, c, ncA); A.compress(w); }
+      if (vB && c < ncB) { uint32_t w[16]; build_tail_chunk(w, data + blkB * bs, sB, c, ncB); B.compress(w); }
+    }
+  }
+  if (vA) A.store(digests + blkA * 20);
+  if (vB) B.store(digests + blkB * 20);
+}
+#endif
+
 // Many equal-size files in ONE launch with their blocks_hash chains.
 // `rows` files of `cols` full-size blocks.  Workgroups [0, chain_wgs) are
 // chain workgroups: each wave owns 64 files and runs chain_wave over S
