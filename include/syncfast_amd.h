@@ -130,6 +130,23 @@ int sf_index_buffer(const uint8_t *data, uint64_t len, uint32_t block_size,
 int sf_index_file(const char *path, uint32_t block_size, sf_block_sig *out, uint64_t cap,
                   uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
 
+/* Many files from disk: what index_path (src/index.rs:685-715) does by calling
+ * index_file (src/index.rs:610-659) once per file, as ONE pipeline.  Fixed
+ * tiling of every file.  Files are packed at 16-B aligned offsets into pinned
+ * stages of about stage_bytes (0 = 256 MiB) by a pool of pread threads; each
+ * stage is copied to HBM and hashed (blocks + every file's blocks_hash,
+ * src/index.rs:661-682) while the next stage is read.  A file larger than a
+ * stage goes through the one-file pipeline of sf_index_file.
+ * out: the rows of file 0, then file 1, ... (offsets relative to each file);
+ * first_row (n_files+1 entries): where each file's rows start;
+ * blocks_hashes: 20 B per file.  *n_out = total rows (the need, with
+ * SF_ENOSPC, checked before any file is read).  On SF_EIO (open, stat or a
+ * short read: the file changed while being indexed) *bad_file (may be NULL)
+ * is the index of the failing file.  Blocking. */
+int sf_index_files(const char *const *paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes,
+                   sf_block_sig *out, uint64_t cap, uint64_t *first_row, uint8_t *blocks_hashes,
+                   uint64_t *n_out, uint32_t *bad_file);
+
 /* compute_blocks_hash (src/index.rs:661-682) on the host: SHA-1 over the
  * n 20-byte digests in order.  Sequential by definition; runs on a host
  * core (SHA-NI when the CPU has it). */

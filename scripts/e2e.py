@@ -55,6 +55,54 @@ def main():
                   rate(n, t), flush=True)
     finally:
         os.unlink(path)
+    many_files(data, d)
+
+
+def many_files(data, d):
+    """index_path's shape: many files from the page cache, (a) through the
+    one native pipeline sf_index_files, (b) one sf_index_file per file (the
+    reference's per-file structure), (c) Index.index_path incl. SQLite rows."""
+    import shutil
+    from syncfast_amd.index import FixedChunker, Index
+    rng = np.random.default_rng(1)
+    cases = [("config-3 shape, 8 MiB files", [8 << 20] * (data.size // (8 << 20))),
+             ("mixed 0-200 KiB files", [])]
+    left = data.size
+    while left > 200 << 10:
+        k = int(rng.integers(0, 200 << 10))
+        cases[1][1].append(k)
+        left -= k
+    for name, sizes in cases:
+        root = tempfile.mkdtemp(dir=d)
+        try:
+            paths, off = [], 0
+            for i, k in enumerate(sizes):
+                p = os.path.join(root, f"f{i:06d}")
+                with open(p, "wb") as f:
+                    f.write(data[off:off + k].tobytes())
+                paths.append(p)
+                off += k
+            total = off
+            host.index_files(paths[:8], 4096)  # warm up
+            t0 = time.perf_counter()
+            rows, first, fh = host.index_files(paths, 4096)
+            ta = time.perf_counter() - t0
+            print(f"sf_index_files {len(paths)} {name} ({total / GiB:.2f} GiB), rows + blocks_hash:",
+                  rate(total, ta), flush=True)
+            t0 = time.perf_counter()
+            for k, p in enumerate(paths):
+                r1, bh1 = host.index_file(p, 4096)
+            tb = time.perf_counter() - t0
+            assert r1.tobytes() == rows[int(first[-2]):].tobytes() and bh1 == bytes(fh[-1])
+            print(f"  one sf_index_file per file: {rate(total, tb)}  -> pipeline x{tb / ta:.1f}", flush=True)
+            idx = Index.open(os.path.join(root, ".syncfast.idx"), chunker=FixedChunker(4096))
+            t0 = time.perf_counter()
+            idx.index_path(root)
+            idx.commit()
+            tc = time.perf_counter() - t0
+            print(f"  Index.index_path (walk + pipeline + SQLite rows): {rate(total, tc)}", flush=True)
+        finally:
+            shutil.rmtree(root)
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@ MAX_BLOCK_SIZE = 32 << 20
 EXPORTED = (
     "sf_version", "sf_strerror", "sf_device_count", "sf_set_device",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
-    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_index_buffer", "sf_index_file",
+    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_index_buffer", "sf_index_file", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
 )
 
@@ -72,6 +72,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]
     L.sf_index_buffer.argtypes = [vp, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
     L.sf_index_file.argtypes = [ctypes.c_char_p, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
+    L.sf_index_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), u32, u32, u64, ctypes.POINTER(BlockSig), u64,
+                                 pu64, vp, pu64, ctypes.POINTER(ctypes.c_uint32)]
     L.sf_blocks_hash.argtypes = [vp, u64, vp]
     L.sf_blocks_hash_sigs.argtypes = [ctypes.POINTER(BlockSig), u64, vp]
     L.sf_sha1_host.argtypes = [vp, u64, vp]

@@ -7,11 +7,13 @@
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <stdint.h>
+#include <sys/stat.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -535,6 +537,192 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   });
   close(fd);
   if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
+  return rc;
+}
+
+// ---- sf_index_files: many files, one pipeline ----------------------------
+
+namespace {
+
+struct FileStage {
+  std::vector<uint32_t> files;    // file indices, in order
+  std::vector<sf_file_desc> desc;  // where each file sits in the stage buffer
+  uint64_t bytes = 0;              // stage buffer bytes (16-B aligned slots)
+  uint64_t rows = 0;
+};
+
+// Fill `dst` with the stage's files: (file, <=16 MiB slice) work items taken
+// by up to 8 threads from an atomic counter.
+int read_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, uint8_t* dst,
+               std::atomic<int64_t>& bad) {
+  constexpr uint64_t kSlice = 16ull << 20;
+  struct Item { uint32_t k; uint64_t a, b; };
+  std::vector<Item> items;
+  for (uint32_t k = 0; k < st.files.size(); k++) {
+    const uint64_t n = size[st.files[k]];
+    for (uint64_t a = 0; a < n; a += kSlice) items.push_back({k, a, std::min(n, a + kSlice)});
+  }
+  std::atomic<size_t> next{0};
+  std::atomic<int> rc{SF_OK};
+  auto worker = [&] {
+    for (size_t i; (i = next.fetch_add(1)) < items.size() && rc.load() == SF_OK;) {
+      const Item& it = items[i];
+      const uint32_t f = st.files[it.k];
+      const int fd = open(paths[f], O_RDONLY);
+      bool ok = fd >= 0;
+      uint8_t* d = dst + st.desc[it.k].offset;
+      for (uint64_t got = it.a; ok && got < it.b;) {
+        const ssize_t r = pread(fd, d + got, it.b - got, (off_t)got);
+        if (r <= 0) ok = false;  // error, or EOF before the size stat() gave
+        else got += (uint64_t)r;
+      }
+      if (fd >= 0) close(fd);
+      if (!ok) {
+        int64_t want = -1;
+        bad.compare_exchange_strong(want, (int64_t)f);
+        rc.store(SF_EIO);
+      }
+    }
+  };
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nthreads = (unsigned)std::min<size_t>(std::min(8u, hw), std::max<size_t>(1, items.size()));
+  std::vector<std::thread> pool;
+  for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  return rc.load();
+}
+
+}  // namespace
+
+int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes_hint,
+                   sf_block_sig* out, uint64_t cap, uint64_t* first_row, uint8_t* blocks_hashes, uint64_t* n_out,
+                   uint32_t* bad_file) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (n_files && (!paths || !first_row || !blocks_hashes)) return SF_EINVAL;
+  const uint32_t bs = block_size;
+  auto fail = [&](uint32_t f, int code) {
+    if (bad_file) *bad_file = f;
+    return code;
+  };
+  // 1. Sizes and the row plan (ENOSPC before any file is read).
+  std::vector<uint64_t> size(n_files);
+  uint64_t total = 0;
+  for (uint32_t f = 0; f < n_files; f++) {
+    if (!paths[f]) return fail(f, SF_EINVAL);
+    struct stat sb;
+    if (stat(paths[f], &sb) != 0 || !S_ISREG(sb.st_mode)) return fail(f, SF_EIO);
+    size[f] = (uint64_t)sb.st_size;
+    first_row[f] = total;
+    total += size[f] ? ceil_div(size[f], bs) : 0;
+  }
+  if (n_files) first_row[n_files] = total;
+  if (n_out) *n_out = total;
+  if (total > cap) return SF_ENOSPC;
+  if (total && !out) return SF_EINVAL;
+  if (n_files == 0) return SF_OK;
+
+  // 2. Stages: consecutive files packed at 16-B aligned offsets (the LDS
+  // path) up to the stage size; larger files go through sf_index_file.
+  const uint64_t stage = stage_bytes_hint ? ((stage_bytes_hint + 15) & ~15ull) : (256ull << 20);
+  std::vector<FileStage> stages;
+  std::vector<uint32_t> big;
+  for (uint32_t f = 0; f < n_files; f++) {
+    const uint64_t slot = (size[f] + 15) & ~15ull;
+    if (size[f] > stage) {
+      big.push_back(f);
+      continue;
+    }
+    if (stages.empty() || stages.back().bytes + slot > stage) stages.emplace_back();
+    FileStage& st = stages.back();
+    st.files.push_back(f);
+    st.desc.push_back({st.bytes, size[f]});
+    st.bytes += slot;
+    st.rows += size[f] ? ceil_div(size[f], bs) : 0;
+  }
+  for (uint32_t f : big) {
+    const uint64_t want = first_row[f + 1] - first_row[f];
+    uint64_t got = 0;
+    rc = sf_index_file(paths[f], bs, out + first_row[f], want, &got, blocks_hashes + 20ull * f);
+    if (rc == SF_ENOSPC || (rc == SF_OK && got != want)) return fail(f, SF_EIO);  // changed meanwhile
+    if (rc) return rc == SF_EIO ? fail(f, rc) : rc;
+  }
+  if (stages.empty()) return SF_OK;
+
+  // 3. Pipeline: read stage k (host threads) while stage k-1 copies and
+  // hashes on its own stream; harvest a stage's rows when its buffer is
+  // reused or at the end.
+  uint64_t max_bytes = 16, max_rows = 1, max_files = 1;
+  for (const FileStage& st : stages) {
+    max_bytes = std::max(max_bytes, st.bytes);
+    max_rows = std::max(max_rows, st.rows);
+    max_files = std::max<uint64_t>(max_files, st.files.size());
+  }
+  Streams sts;
+  DevBuf ddata[2], ddig[2], dfh[2];
+  PinBuf pin[2], pdig[2], pfh[2];
+  for (int i = 0; i < 2; i++) {
+    SF_HIP(hipStreamCreateWithFlags(&sts.s[i], hipStreamNonBlocking));
+    SF_HIP(hipMalloc(&ddata[i].p, max_bytes));
+    SF_HIP(hipMalloc(&ddig[i].p, max_rows * 20));
+    SF_HIP(hipMalloc(&dfh[i].p, max_files * 20));
+    SF_HIP(hipHostMalloc(&pin[i].p, std::min<uint64_t>(max_bytes, stage), hipHostMallocDefault));
+    SF_HIP(hipHostMalloc(&pdig[i].p, max_rows * 20, hipHostMallocDefault));
+    SF_HIP(hipHostMalloc(&pfh[i].p, max_files * 20, hipHostMallocDefault));
+  }
+  hipEvent_t done[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  auto harvest = [&](size_t k) {
+    const FileStage& st = stages[k];
+    const int b = (int)(k & 1);
+    const uint8_t* dg = static_cast<const uint8_t*>(pdig[b].p);
+    const uint8_t* fh = static_cast<const uint8_t*>(pfh[b].p);
+    uint64_t r = 0;
+    for (size_t j = 0; j < st.files.size(); j++) {
+      const uint32_t f = st.files[j];
+      sf_block_sig* o = out + first_row[f];
+      const uint64_t nb = first_row[f + 1] - first_row[f];
+      for (uint64_t i = 0; i < nb; i++, r++) {
+        o[i].offset = i * bs;
+        o[i].size = (uint32_t)std::min<uint64_t>(bs, size[f] - i * bs);
+        memcpy(o[i].sha1, dg + 20 * r, 20);
+      }
+      memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
+    }
+  };
+  std::atomic<int64_t> bad{-1};
+  for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    const FileStage& st = stages[k];
+    if (k >= 2) {
+      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+      harvest(k - 2);
+    }
+    rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad);
+    if (rc) break;
+    hipStream_t s = sts.s[b];
+    if (st.bytes && hipMemcpyAsync(ddata[b].p, pin[b].p, st.bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+    uint64_t nb = 0;
+    rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
+                               max_rows, dfh[b].p, nullptr, &nb, s);
+    if (rc) break;
+    if ((nb && hipMemcpyAsync(pdig[b].p, ddig[b].p, nb * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipMemcpyAsync(pfh[b].p, dfh[b].p, st.files.size() * 20, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(done[b], s) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+  }
+  for (int i = 0; i < 2; i++)
+    if (hipStreamSynchronize(sts.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  if (rc == SF_OK)
+    for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size(); k++) harvest(k);
+  for (int i = 0; i < 2; i++) (void)hipEventDestroy(done[i]);
+  if (rc == SF_EIO && bad.load() >= 0) return fail((uint32_t)bad.load(), rc);
   return rc;
 }
 

@@ -9,11 +9,11 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Tuple
+from typing import List, Sequence, Tuple
 
 import numpy as np
 
-from ._lib import BlockSig, check, lib
+from ._lib import SF_EINVAL, SF_EIO, SF_ENOSPC, BlockSig, check, lib
 
 SIG_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("sha1", "u1", (20,))], align=True)
 assert SIG_DTYPE.itemsize == ctypes.sizeof(BlockSig) == 32
@@ -48,6 +48,35 @@ def index_file(path, block_size: int) -> Tuple[np.ndarray, bytes]:
                               n, ctypes.byref(nout), bh),
           "sf_index_file")
     return out[:nout.value], bytes(bh)
+
+
+def index_files(paths: Sequence, block_size: int, stage_bytes: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Many files through one pipeline (sf_index_files): what index_path does
+    with one index_file per file (src/index.rs:685-715, 610-659).
+
+    Returns (rows, first_row, blocks_hashes): file k's rows are
+    rows[first_row[k]:first_row[k+1]] (offsets relative to the file), its
+    blocks_hash is blocks_hashes[k] (uint8[20]).  stage_bytes = 0 uses the
+    library default (256 MiB).  An unreadable file raises SfError naming it."""
+    n = len(paths)
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(n, 1))(*enc)
+    first = np.zeros(n + 1, np.uint64)
+    hashes = np.zeros((max(n, 1), 20), np.uint8)
+    need, bad = ctypes.c_uint64(0), ctypes.c_uint32(0)
+    cap = 0
+    while True:  # a file may grow between the sizing call and the real one
+        out = np.zeros(max(cap, 1), SIG_DTYPE)
+        rc = lib().sf_index_files(arr, n, block_size, stage_bytes, out.ctypes.data_as(ctypes.POINTER(BlockSig)),
+                                  cap, first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), hashes.ctypes.data,
+                                  ctypes.byref(need), ctypes.byref(bad))
+        if rc == SF_ENOSPC and need.value > cap:
+            cap = need.value
+            continue
+        where = f"sf_index_files: {os.fsdecode(enc[bad.value])}" if rc in (SF_EIO, SF_EINVAL) and bad.value < n \
+            else "sf_index_files"
+        check(rc, where)
+        return out[:need.value], first, hashes[:n]
 
 
 def blocks_hash(digests) -> bytes:

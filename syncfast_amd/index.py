@@ -356,14 +356,15 @@ class Index:
         bh = self.compute_blocks_hash(file_id)
         self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
 
-    def index_path(self, path, batch_bytes: int = 1 << 30) -> None:
+    def index_path(self, path, batch_bytes: int = 256 << 20) -> None:
         """Index files and directories recursively (src/index.rs:685-715).
 
         Same walk, names and mtime gate as the reference.  With a
-        FixedChunker, files that need (re)indexing are hashed in batches of
-        up to `batch_bytes`: one pinned host buffer, one H2D copy and one
-        device launch per batch (blocks + every file's blocks_hash), instead
-        of one pipeline per file.  batch_bytes=0 indexes file by file."""
+        FixedChunker, every file that needs (re)indexing goes through ONE
+        native pipeline (sf_index_files) in stages of `batch_bytes`: pinned
+        host buffers filled by a pread thread pool, one H2D copy and one
+        device launch per stage (blocks + every file's blocks_hash), reading
+        overlapped with the device.  batch_bytes=0 indexes file by file."""
         todo: List[Tuple[Path, PurePath]] = []
         self._index_path_rec(Path(path), PurePath(""), todo)
         if not todo:
@@ -389,42 +390,30 @@ class Index:
             todo.append((p, rel))
 
     def _index_batched(self, todo, batch_bytes: int) -> None:
-        import torch
-        from . import device
+        """Every file needing (re)indexing through ONE native pipeline
+        (sf_index_files): pread thread pool into pinned stages of
+        `batch_bytes`, H2D + device blocks/blocks_hash per stage, overlapped
+        with the reading of the next stage."""
         bs = self.chunker.block_size
-        pending = []  # (file_id, path, size) needing signatures
+        pending = []  # (file_id, path) needing signatures
         for p, rel in todo:
             with open(p, "rb"):  # same error as File::open on a vanished file
                 file_id, up_to_date = self.add_file(rel, _mtime(p))
             if not up_to_date:
-                pending.append((file_id, p, os.path.getsize(p)))
-        i = 0
-        dev = torch.device("cuda", torch.cuda.current_device())
-        while i < len(pending):
-            group, total = [], 0
-            while i < len(pending) and (not group or total + pending[i][2] <= batch_bytes):
-                group.append(pending[i])
-                total += (pending[i][2] + 15) // 16 * 16  # 16-B aligned slots: LDS path
-                i += 1
-            host_buf = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
-            hv = host_buf.numpy()
-            files, off = [], 0
-            for _fid, p, size in group:
-                with open(p, "rb") as f:
-                    got = f.readinto(memoryview(hv[off:off + size]))
-                if got != size:
-                    raise SyncfastError(f"short read on {p}")
-                files.append((off, size))
-                off += (size + 15) // 16 * 16
-            data = host_buf.to(dev, non_blocking=True)
-            dig, first, fh = device.index_device_batch(data, files, bs)
-            dig, fh = dig.cpu().numpy(), fh.cpu().numpy()
-            for k, (file_id, _p, size) in enumerate(group):
-                a, b = int(first[k]), int(first[k + 1])
-                rows = [((j - a) * bs, min(bs, size - (j - a) * bs), bytes(dig[j])) for j in range(a, b)]
-                self.add_blocks(file_id, rows)
-                self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;",
-                                (bytes(fh[k]).hex(), file_id))
+                pending.append((file_id, p))
+        if not pending:
+            return
+        rows, first, fh = host.index_files([p for _f, p in pending], bs, stage_bytes=batch_bytes)
+        # Columns converted once for all files (hex = HashDigest ToSql,
+        # src/lib.rs:78-90), then one executemany per file.
+        hx = rows["sha1"].tobytes().hex()
+        offs, sizes = rows["offset"].tolist(), rows["size"].tolist()
+        fhx = fh.tobytes().hex()
+        ins = "INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);"
+        for k, (file_id, _p) in enumerate(pending):
+            a, b = int(first[k]), int(first[k + 1])
+            self.db.executemany(ins, ((hx[40 * i:40 * i + 40], file_id, offs[i], sizes[i]) for i in range(a, b)))
+            self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
 
     def remove_missing_files(self, path) -> None:
         """src/index.rs:718-726."""

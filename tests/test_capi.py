@@ -64,6 +64,36 @@ def test_argument_validation_without_device():
     assert L.sf_blocks_hash(None, 0, None) == _lib.SF_EINVAL
 
 
+def test_index_files_validation_without_device(tmp_path):
+    """sf_index_files sizes every file and checks capacity before any read or
+    device call: empty list, missing file (named by index), ENOSPC."""
+    L = syncfast_amd.lib()
+    n, bad = ctypes.c_uint64(7), ctypes.c_uint32(99)
+    first = np.zeros(4, np.uint64)
+    fh = np.zeros((3, 20), np.uint8)
+    pfirst = first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    none = (ctypes.c_char_p * 1)()
+    assert L.sf_index_files(none, 0, 4096, 0, None, 0, pfirst, fh.ctypes.data, ctypes.byref(n),
+                            ctypes.byref(bad)) == 0 and n.value == 0
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.write_bytes(b"x" * 5000)
+    b.write_bytes(b"")
+    paths = (ctypes.c_char_p * 3)(bytes(a), b"/nonexistent/file", bytes(b))
+    assert L.sf_index_files(paths, 3, 4096, 0, None, 0, pfirst, fh.ctypes.data, ctypes.byref(n),
+                            ctypes.byref(bad)) == _lib.SF_EIO and bad.value == 1
+    paths = (ctypes.c_char_p * 3)(bytes(a), bytes(b), bytes(tmp_path))  # a directory is not a file
+    assert L.sf_index_files(paths, 3, 4096, 0, None, 0, pfirst, fh.ctypes.data, ctypes.byref(n),
+                            ctypes.byref(bad)) == _lib.SF_EIO and bad.value == 2
+    paths = (ctypes.c_char_p * 3)(bytes(a), bytes(b), bytes(a))
+    assert L.sf_index_files(paths, 3, 4096, 0, None, 3, pfirst, fh.ctypes.data, ctypes.byref(n),
+                            ctypes.byref(bad)) == _lib.SF_ENOSPC and n.value == 4
+    assert first.tolist() == [0, 2, 2, 4]
+    assert L.sf_index_files(paths, 3, 0, 0, None, 9, pfirst, fh.ctypes.data, ctypes.byref(n),
+                            ctypes.byref(bad)) == _lib.SF_EINVAL
+    with pytest.raises(_lib.SfError, match="nonexistent"):
+        host.index_files([a, "/nonexistent/file"], 4096)
+
+
 def test_device_count_is_queryable():
     assert syncfast_amd.device_count() >= 0
 
