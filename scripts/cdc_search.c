@@ -1,0 +1,150 @@
+/* cdc_search.c -- search for a ZPAQ-style rolling-hash recurrence that
+ * reproduces the reference's only CDC known-answer test.
+ *
+ * The reference cuts blocks with cdchunking 0.2.1's ZPAQ(13) + max_size(32768)
+ * (/root/reference/src/index.rs:622-625).  That crate is not vendored, so its
+ * recurrence can only be restated from the published ZPAQ fragmenter and
+ * checked against the KAT of src/index.rs:747-793:
+ *   input  = "Line 1\n" .. "Line 2000\n" + 2000 x "Test content\n" (44,893 B)
+ *   blocks = [0, 11579), [11579, 44347) (forced at 32 KiB), [44347, 44893).
+ * This program enumerates a grammar of variants (multiplier pair, update
+ * form, prediction context, boundary predicate and width, 32/64-bit state,
+ * cut side, reset policy, check order) and prints every variant whose cut
+ * list equals the KAT's, plus every variant that at least reaches the first
+ * cut.  Research tool: nothing in the product or the tests links it.
+ *
+ *   gcc -O2 -o /tmp/cdc_search scripts/cdc_search.c && /tmp/cdc_search
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+static uint8_t buf[64 << 10];
+static int n;
+
+static const uint64_t MPAIRS[][2] = {
+    {314159265u, 271828182u}, {271828182u, 314159265u}, {314159265u, 271828183u},
+    {271828183u, 314159265u}, {3141592653u, 2718281828u}, {2718281828u, 3141592653u},
+};
+#define NPAIRS (int)(sizeof(MPAIRS) / sizeof(MPAIRS[0]))
+
+typedef struct {
+  int mp, form, ctx, pred, k, incl, reset, order, w64;
+} Hyp;
+
+typedef struct {
+  uint64_t h;
+  uint8_t c1;
+  uint8_t o1[256];
+} St;
+
+static void st_reset(St* s, int what) {
+  if (what & 1) s->h = 0;
+  if (what & 2) {
+    s->c1 = 0;
+    memset(s->o1, 0, 256);
+  }
+}
+
+static inline void upd(St* s, const Hyp* y, uint8_t c) {
+  int match;
+  switch (y->ctx) {
+    case 0: match = (c == s->o1[s->c1]); s->o1[s->c1] = c; s->c1 = c; break;
+    case 1: match = (c == s->o1[s->c1]); s->c1 = c; s->o1[s->c1] = c; break;
+    case 2: match = (c == s->c1); s->c1 = c; break;
+    default: match = (c == s->o1[s->c1]); s->c1 = c; break;  /* table never updated */
+  }
+  const uint64_t M = match ? MPAIRS[y->mp][0] : MPAIRS[y->mp][1];
+  uint64_t h = s->h;
+  switch (y->form) {
+    case 0: h = (h + c + 1u) * M; break;
+    case 1: h = h * M + c + 1u; break;
+    case 2: h = (h + c) * M; break;
+    case 3: h = h * M + c; break;
+    case 4: h = (h ^ c) * M; break;
+    case 5: h = (h * M) ^ c; break;
+    default: h = (h + c + 1u) * M; h ^= h >> (y->w64 ? 32 : 16); break;
+  }
+  s->h = y->w64 ? h : (uint32_t)h;
+}
+
+/* k = predicate width in bits; B = state bits (32 or 64). */
+static inline int pred(const Hyp* y, uint64_t h) {
+  const int B = y->w64 ? 64 : 32;
+  const uint64_t k = (uint64_t)y->k;
+  const uint64_t m = (1ull << k) - 1u;
+  const uint64_t top = y->w64 ? ~0ull : 0xFFFFFFFFull;
+  switch (y->pred) {
+    case 0: return h < (1ull << k);                     /* h < 2^k */
+    case 1: return (h & m) == 0;                        /* low k bits zero */
+    case 2: return (h >> (B - k)) == m;                 /* top k bits all ones */
+    case 3: return (h & m) == m;                        /* low k bits all ones */
+    case 4: return h <= (1ull << k);
+    default: return h > top - (1ull << k);              /* near the top */
+  }
+}
+
+/* Run the chunker; returns 1 iff cuts == {11579, 44347, n}.  *first = first cut. */
+static int run(const Hyp* y, int* first) {
+  static const int want[3] = {11579, 44347, 44893};
+  St s;
+  memset(&s, 0, sizeof s);
+  int start = 0, ncut = 0, i = 0;
+  *first = -1;
+  while (i < n) {
+    int cut = -1, forced = 0;
+    if (y->order == 1 && i > start && pred(y, s.h)) {
+      cut = i;  /* state after byte i-1 satisfied the predicate: cut before byte i */
+    } else {
+      upd(&s, y, buf[i]);
+      if (y->order == 0 && pred(y, s.h)) cut = y->incl ? i + 1 : i;
+      if (cut == start) cut = -1;  /* never an empty chunk */
+      if (cut < 0 && i + 1 - start >= 32768) { cut = i + 1; forced = 1; }
+    }
+    if (cut < 0) { ++i; continue; }
+    if (*first < 0) *first = cut;
+    if (ncut >= 2 || cut != want[ncut]) return 0;
+    ++ncut;
+    start = cut;
+    if (!forced || (y->reset & 4)) st_reset(&s, y->reset & 3);
+    i = cut;  /* bytes from the cut on are fed to the fresh chunk */
+    if (y->order == 0 && !y->incl && !forced && !(y->reset & 8)) i = cut + 1;  /* trigger byte not re-fed */
+  }
+  return ncut == 2;
+}
+
+int main(void) {
+  n = 0;
+  for (int i = 1; i <= 2000; ++i) n += sprintf((char*)buf + n, "Line %d\n", i);
+  for (int i = 0; i < 2000; ++i) n += sprintf((char*)buf + n, "Test content\n");
+  if (n != 44893) { fprintf(stderr, "bad KAT length %d\n", n); return 1; }
+  long tried = 0, first_ok = 0, full = 0;
+  Hyp y;
+  for (y.w64 = 0; y.w64 < 2; ++y.w64)
+  for (y.mp = 0; y.mp < NPAIRS; ++y.mp)
+  for (y.form = 0; y.form < 7; ++y.form)
+  for (y.ctx = 0; y.ctx < 4; ++y.ctx)
+  for (y.pred = 0; y.pred < 6; ++y.pred)
+  for (y.k = 1; y.k <= (y.w64 ? 63 : 31); ++y.k)
+  for (y.order = 0; y.order < 2; ++y.order)
+  for (y.incl = 0; y.incl < 2; ++y.incl)
+  for (y.reset = 0; y.reset < 16; ++y.reset) {
+    if (y.order == 1 && y.incl == 0) continue;  /* order 1 has one cut side */
+    int f;
+    ++tried;
+    const int ok = run(&y, &f);
+    if (f == 11579) {
+      ++first_ok;
+      printf("%s w64=%d mp=%d form=%d ctx=%d pred=%d k=%d order=%d incl=%d reset=%d\n", ok ? "FULL " : "first",
+             y.w64, y.mp, y.form, y.ctx, y.pred, y.k, y.order, y.incl, y.reset);
+    }
+    full += ok;
+  }
+  /* The survey's restatement, for the record. */
+  Hyp z = {0, 0, 0, 0, 19, 1, 3, 0, 0};
+  int f;
+  run(&z, &f);
+  printf("tried %ld variants: %ld reach the first cut 11579, %ld match all cuts; "
+         "zpaq form (h+c+1)*M, h<2^19 -> first cut %d\n", tried, first_ok, full, f);
+  return 0;
+}
