@@ -91,6 +91,19 @@ int sf_index_device_blocks(const void *d_data, uint64_t len, const uint64_t *d_o
                            const uint32_t *d_sizes, uint64_t n_blocks, void *d_digests,
                            int *d_status, void *stream);
 
+/* Opt-in weak checksum -- NOT part of the reference (SURVEY.md 8a row a8:
+ * syncfast stores and sends no weak sum); north_star names an "Adler32-style"
+ * weak sum beside the strong hash.  As sf_index_device_fixed /
+ * sf_index_device_blocks, plus d_weak[i] = zlib Adler-32 (RFC 1950) of block
+ * i's bytes, fused into the same pass over HBM (uint32 per block; 0 for an
+ * out-of-range explicit block). */
+int sf_index_device_fixed_weak(const void *d_data, uint64_t len, uint32_t block_size,
+                               void *d_digests, uint32_t *d_weak, uint64_t cap_blocks,
+                               uint64_t *n_blocks, void *stream);
+int sf_index_device_blocks_weak(const void *d_data, uint64_t len, const uint64_t *d_offsets,
+                                const uint32_t *d_sizes, uint64_t n_blocks, void *d_digests,
+                                uint32_t *d_weak, int *d_status, void *stream);
+
 /* Many-file batch: files[] (host array) describes n_files files inside
  * d_data[0, len).  Writes every file's fixed-size block digests, file after
  * file, to d_digests (cap_blocks rows) and, if d_file_hashes != NULL, each

@@ -58,6 +58,10 @@ def lib() -> ctypes.CDLL:
         L.sfo_index_fixed_mt.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_int]
         L.sfo_index_fixed_mt.restype = ctypes.c_uint64
         L.sfo_fill_splitmix.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.sfo_adler32.argtypes = [u8p, ctypes.c_uint64]
+        L.sfo_adler32.restype = ctypes.c_uint32
+        L.sfo_adler_fixed.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, u8p]
+        L.sfo_adler_blocks.argtypes = [u8p, u8p, u8p, ctypes.c_uint64, u8p]
         _lib = L
     return _lib
 
@@ -118,6 +122,29 @@ def blocks_hash(digests) -> bytes:
     out = np.zeros(20, np.uint8)
     lib().sfo_blocks_hash(_ptr(d), d.size // 20, _ptr(out))
     return out.tobytes()
+
+
+def adler32(data) -> int:
+    """zlib Adler-32 of a byte range (checker for the opt-in weak sum)."""
+    a = _as_u8(data)
+    return int(lib().sfo_adler32(_ptr(a), a.size))
+
+
+def adler_fixed(data, block_size: int) -> np.ndarray:
+    a = _as_u8(data)
+    n = lib().sfo_num_blocks(a.size, block_size)
+    out = np.zeros(n, np.uint32)
+    lib().sfo_adler_fixed(_ptr(a), a.size, block_size, _ptr(out))
+    return out
+
+
+def adler_blocks(data, offsets, sizes) -> np.ndarray:
+    a = _as_u8(data)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sz = np.ascontiguousarray(sizes, dtype=np.uint32)
+    out = np.zeros(offs.size, np.uint32)
+    lib().sfo_adler_blocks(_ptr(a), _ptr(offs), _ptr(sz), offs.size, _ptr(out))
+    return out
 
 
 def splitmix_bytes(length: int, seed: int, start: int = 0) -> np.ndarray:

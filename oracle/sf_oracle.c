@@ -148,6 +148,34 @@ void sfo_blocks_hash(const uint8_t *digests, uint64_t n, uint8_t out[20]) {
     sfo_sha1(digests, n * 20u, out);
 }
 
+/* ------------------------------------ opt-in weak sum (not in reference) */
+
+/* zlib Adler-32 (RFC 1950 section 9) of one byte range: the checker for the
+ * product's opt-in fused weak sum.  The reference computes no weak sum
+ * (SURVEY.md 8a row a8); zlib.adler32 cross-checks this in tests/. */
+uint32_t sfo_adler32(const uint8_t *data, uint64_t len) {
+    uint64_t a = 1, b = 0;
+    for (uint64_t i = 0; i < len; i++) {
+        a += data[i];
+        b += a;
+        if ((i & 4095) == 4095) { a %= 65521u; b %= 65521u; }
+    }
+    return (uint32_t)(((b % 65521u) << 16) | (a % 65521u));
+}
+
+void sfo_adler_fixed(const uint8_t *data, uint64_t len, uint64_t block_size, uint32_t *out) {
+    uint64_t n = sfo_num_blocks(len, block_size);
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t off = i * block_size;
+        out[i] = sfo_adler32(data + off, len - off < block_size ? len - off : block_size);
+    }
+}
+
+void sfo_adler_blocks(const uint8_t *data, const uint64_t *offsets, const uint32_t *sizes, uint64_t n,
+                      uint32_t *out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = sfo_adler32(data + offsets[i], sizes[i]);
+}
+
 /* ---------------------------------------- multi-threaded CPU baseline */
 
 typedef struct {

@@ -76,46 +76,56 @@ sf::PadSchedule pad_schedule(uint32_t bytes) {
 }
 
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
-                 hipStream_t stream) {
+                 hipStream_t stream, uint32_t* weak = nullptr) {
   if (nblocks == 0) return SF_OK;
   const unsigned grid = grid_for_blocks(nblocks);
   const sf::PadSchedule pad = pad_schedule(bs);
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
   uint8_t* o = static_cast<uint8_t*>(d_digests);
+  if (weak) {  // opt-in fused Adler-32 (a separate instantiation; the default kernel is unchanged)
+    hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1, true>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs,
+                       nblocks, o, pad, weak);
+    return hip_err(hipGetLastError());
+  }
 #ifdef SF_TUNING
   // Tuning builds only (make variant EXTRA=-DSF_TUNING): SF_VARIANT selects a
   // (tile, waves-per-SIMD) instantiation for interleaved A/B in one process.
   switch (variant_choice()) {
-    case 1: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 5>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 3: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 8>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 5: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 4>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 6: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 2>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
-    case 7: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 3>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    case 1: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 5>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 3: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 8>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 5: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 4>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 6: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 2>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
+    case 7: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 3>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
     case 8:
       if (bs % 64 == 0 && (reinterpret_cast<uintptr_t>(d) & 15u) == 0) {
         hipLaunchKernelGGL(sf::sha1_fixed2_kernel, dim3((unsigned)ceil_div(ceil_div(nblocks, 128), sf::kWavesPerWG)),
                            dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
         break;
       }
-      hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
+      hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
       break;
-    default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad); break;
+    default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
   }
 #else
-  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
+  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
 #endif
   return hip_err(hipGetLastError());
 }
 
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
-                 uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream) {
+                 uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr) {
   if (nblocks == 0) return SF_OK;
   const unsigned grid = grid_for_blocks(nblocks);
-  hipLaunchKernelGGL(sf::sha1_table_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, stream,
-                     static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                     static_cast<uint8_t*>(d_digests), d_status);
+  if (weak)
+    hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, true>), dim3(grid), dim3(sf::kThreads), 0, stream,
+                       static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
+                       static_cast<uint8_t*>(d_digests), d_status, weak);
+  else
+    hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, false>), dim3(grid), dim3(sf::kThreads), 0, stream,
+                       static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
+                       static_cast<uint8_t*>(d_digests), d_status, nullptr);
   return hip_err(hipGetLastError());
 }
 
@@ -296,6 +306,24 @@ int sf_index_device_blocks(const void* d_data, uint64_t len, const uint64_t* d_o
   // empty and the kernel dereferences nothing).
   if (!d_offsets || !d_sizes || !d_digests || (!d_data && len)) return SF_EINVAL;
   return launch_table(d_data, len, d_offsets, d_sizes, n_blocks, d_digests, d_status, as_stream(stream));
+}
+
+int sf_index_device_fixed_weak(const void* d_data, uint64_t len, uint32_t block_size, void* d_digests,
+                               uint32_t* d_weak, uint64_t cap_blocks, uint64_t* n_blocks, void* stream) {
+  int rc = check_fixed_args(len, block_size);
+  if (rc) return rc;
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_blocks) *n_blocks = nb;
+  if (nb > cap_blocks) return SF_ENOSPC;
+  if (nb && (!d_data || !d_digests || !d_weak)) return SF_EINVAL;
+  return launch_fixed(d_data, len, block_size, nb, d_digests, as_stream(stream), d_weak);
+}
+
+int sf_index_device_blocks_weak(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
+                                uint64_t n_blocks, void* d_digests, uint32_t* d_weak, int* d_status, void* stream) {
+  if (n_blocks == 0) return SF_OK;
+  if (!d_offsets || !d_sizes || !d_digests || !d_weak || (!d_data && len)) return SF_EINVAL;
+  return launch_table(d_data, len, d_offsets, d_sizes, n_blocks, d_digests, d_status, as_stream(stream), d_weak);
 }
 
 int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,

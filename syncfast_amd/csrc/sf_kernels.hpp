@@ -151,11 +151,13 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
 
 // Hash the block (off, size) owned by this lane; all 64 lanes of the wave
 // enter together.  `rel` = off - geo.base (valid lanes).  TILE = bytes of
-// each block staged per LDS step.
-template <int TILE, bool HAS_PAD>
+// each block staged per LDS step.  WEAK: also fold the same words into the
+// lane's Adler-32 (opt-in weak sum, sha1_device.hpp).
+template <int TILE, bool HAS_PAD, bool WEAK = false>
 __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
                                           uint32_t rel, bool valid, const WaveGeo& geo,
-                                          uint4* __restrict__ wave_tile, Sha1& st, const PadSchedule pad) {
+                                          uint4* __restrict__ wave_tile, Sha1& st, const PadSchedule pad,
+                                          Adler& wk) {
   constexpr int PIECES = TILE / 16;           // 16-B pieces per block per step
   constexpr int CH = TILE / 64;               // compressions per step
   constexpr int GSHIFT = PIECES == 4 ? 2 : (PIECES == 8 ? 1 : 0);
@@ -164,6 +166,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
   const int lane = threadIdx.x & 63;
 
   st.init();
+  if constexpr (WEAK) wk.init();
   const uint32_t nfull = geo.min_size / 64u;
   uint32_t c_done = 0;
   if (geo.lds_ok) {
@@ -227,6 +230,18 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
           w[4 * q + 2] = bswap32(v.z);
           w[4 * q + 3] = bswap32(v.w);
         }
+        if constexpr (WEAK) {
+          uint32_t le[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 v = raw[ch * 4 + q];
+            le[4 * q + 0] = v.x;
+            le[4 * q + 1] = v.y;
+            le[4 * q + 2] = v.z;
+            le[4 * q + 3] = v.w;
+          }
+          wk.chunk(le);
+        }
         st.compress(w);
       }
     }
@@ -235,12 +250,31 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     // Misaligned or > 4 GiB span: each lane streams its own block.
     const uint8_t* p = data + off;
     for (uint32_t c = 0; c < nfull; ++c) {
-      uint32_t w[16];
+      uint32_t le[16], w[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = bswap32(ld_u32_any(p + (uint64_t)c * 64 + 4 * j));
+      for (int j = 0; j < 16; ++j) {
+        le[j] = ld_u32_any(p + (uint64_t)c * 64 + 4 * j);
+        w[j] = bswap32(le[j]);
+      }
+      if constexpr (WEAK) wk.chunk(le);
       st.compress(w);
     }
     c_done = nfull;
+  }
+  // Weak sum of this lane's bytes past the chunks both paths consumed
+  // (whole chunks, then < 64 single bytes); never reads outside the block.
+  if constexpr (WEAK) {
+    if (valid) {
+      const uint8_t* p = data + off;
+      const uint32_t full = size / 64u;
+      for (uint32_t c = c_done; c < full; ++c) {
+        uint32_t le[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) le[j] = ld_u32_any(p + (uint64_t)c * 64 + 4 * j);
+        wk.chunk(le);
+      }
+      for (uint32_t i = full * 64u; i < size; ++i) wk.byte(p[i]);
+    }
   }
   // Every block of the wave has the same 64-B multiple size and all its data
   // chunks are done: the last chunk is the same padding for every lane.
@@ -266,10 +300,10 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 // Fixed tiling: block i = data[i*bs, min((i+1)*bs, len)).
 // WPE = minimum resident waves per SIMD requested from the register
 // allocator (__launch_bounds__ 2nd argument, per EU on gfx950).
-template <int TILE, int WPE = 1>
+template <int TILE, int WPE = 1, bool WEAK = false>
 __global__ void __launch_bounds__(kThreads, WPE)
 sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                  uint8_t* __restrict__ digests, const PadSchedule pad) {
+                  uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
@@ -293,8 +327,12 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
   const uint32_t rel = (uint32_t)((uint64_t)lane * bs);
 
   Sha1 st;
-  hash_wave<TILE, true>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
-  if (valid) st.store(digests + blk * 20);
+  Adler wk;
+  hash_wave<TILE, true, WEAK>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad, wk);
+  if (valid) {
+    st.store(digests + blk * 20);
+    if constexpr (WEAK) weak[blk] = wk.fin();
+  }
 }
 
 // Stream a 64-B-multiple byte range [lo, hi) of a lane's message through
@@ -517,7 +555,8 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
                geo.span < 0xF0000000ull;
   const uint32_t rel = (uint32_t)(off - geo.base);
   Sha1 st;
-  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad);
+  Adler wk;  // unused (no weak sum in the staged batch)
+  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad, wk);
   if (chain_wgs == 0 && file_hashes == nullptr) {  // experiment: blocks only, no publish
     if (valid) st.store(digests + (row * out_stride + col) * 20);
     return;
@@ -535,11 +574,11 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
 // many-file batches, and (over the digest table) per-file blocks_hash.
 // A block outside [0, len) is not read: its digest is zeroed and *status is
 // set to -34 (SF_ERANGE).
-template <int TILE>
+template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(kThreads)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
-                  int* __restrict__ status) {
+                  int* __restrict__ status, uint32_t* __restrict__ weak) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -573,14 +612,18 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 
   Sha1 st;
-  hash_wave<TILE, false>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, PadSchedule{});
+  Adler wk;
+  hash_wave<TILE, false, WEAK>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, PadSchedule{},
+                               wk);
   if (valid) {
     if (bad) {
       uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);
       o[0] = o[1] = o[2] = o[3] = o[4] = 0;
+      if constexpr (WEAK) weak[blk] = 0u;
       if (status) *status = -34;
     } else {
       st.store(digests + blk * 20);
+      if constexpr (WEAK) weak[blk] = wk.fin();
     }
   }
 }

@@ -129,4 +129,45 @@ struct Sha1 {
   }
 };
 
+// Weak per-block checksum: zlib Adler-32 (RFC 1950 s.9), NOT computed by the
+// reference (no table, message or call site carries a
+// weak sum); north_star asks for an "Adler32-style" weak sum beside the strong
+// hash, so the kernels can fuse one as an opt-in second output.
+//   A = 1 + sum(x_i),  B = sum over i of A after byte i  (both mod 65521).
+// Per 64-B chunk of bytes x_0..x_63 (memory order): A += S1, B += 64*A + S2
+// with S1 = sum x_i, S2 = sum (64 - i) x_i -- two v_dot4_u32_u8 per word.
+// Between chunks A and B stay partially reduced (65536 = 15 mod 65521):
+// a <= 65550 and b <= 66720 hold after every chunk, so nothing overflows 32
+// bits for any block length; fin() reduces exactly.
+struct Adler {
+  uint32_t a, b;
+  __device__ __forceinline__ void init() { a = 1u; b = 0u; }
+  __device__ __forceinline__ static uint32_t fold(uint32_t x) { return (x & 0xFFFFu) + (x >> 16) * 15u; }
+  // 16 little-endian words = the chunk's 64 bytes in memory order.
+  __device__ __forceinline__ void chunk(const uint32_t (&le)[16]) {
+    uint32_t s1 = 0u, s2 = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // byte k of word j is x_{4j+k}: weight 64 - 4j - k
+      const uint32_t wt = (uint32_t)(64 - 4 * j) | ((uint32_t)(63 - 4 * j) << 8) |
+                          ((uint32_t)(62 - 4 * j) << 16) | ((uint32_t)(61 - 4 * j) << 24);
+      s1 = __builtin_amdgcn_udot4(le[j], 0x01010101u, s1, false);
+      s2 = __builtin_amdgcn_udot4(le[j], wt, s2, false);
+    }
+    b = fold(b + (a << 6) + s2);  // < 66720 + 64 * 65550 + 530400 before the fold
+    a = fold(a + s1);
+  }
+  // One trailing byte (fewer than 64 follow the last chunk()).
+  __device__ __forceinline__ void byte(uint32_t x) {
+    a += x;
+    b += a;
+  }
+  __device__ __forceinline__ uint32_t fin() const {
+    uint32_t A = fold(a), B = fold(b);
+    A = A >= 65521u ? A - 65521u : A;
+    B = B >= 65521u ? B - 65521u : B;
+    return (B << 16) | A;
+  }
+};
+
 }  // namespace sf

@@ -24,6 +24,7 @@ from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
 
 __all__ = [
     "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
+    "index_device_weak", "index_device_blocks_weak",
     "fill_splitmix", "splitmix_tensor",
 ]
 
@@ -99,6 +100,58 @@ def index_device_blocks(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.
     if status is not None and int(status.item()) != 0:
         raise SfError(SF_ERANGE, "sf_index_device_blocks")
     return out
+
+
+def index_device_weak(data: torch.Tensor, block_size: int, out: Optional[torch.Tensor] = None,
+                      weak_out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None):
+    """index_device plus the opt-in weak sum: (digests uint8[n, 20], weak
+    int32[n]) where weak[i] is the zlib Adler-32 of block i (bit pattern of
+    the uint32), fused into the same kernel pass.  Not in the reference
+    (SURVEY.md 8a row a8)."""
+    _require_device(data, "data", torch.uint8)
+    n = num_blocks(data.numel(), block_size)
+    if out is None:
+        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+    if weak_out is None:
+        weak_out = torch.empty(n, dtype=torch.int32, device=data.device)
+    _require_device(out, "out", torch.uint8)
+    _require_device(weak_out, "weak_out", torch.int32)
+    if out.numel() < 20 * n or weak_out.numel() < n:
+        raise ValueError(f"outputs too small for {n} blocks")
+    nb = ctypes.c_uint64(0)
+    with torch.cuda.device(data.device):
+        check(lib().sf_index_device_fixed_weak(data.data_ptr() if data.numel() else None, data.numel(), block_size,
+                                               out.data_ptr() if n else None, weak_out.data_ptr() if n else None,
+                                               min(out.numel() // 20, weak_out.numel()), ctypes.byref(nb),
+                                               _stream_ptr(data, stream)),
+              "sf_index_device_fixed_weak")
+    return out, weak_out
+
+
+def index_device_blocks_weak(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                             check_range: bool = True, stream: Optional[torch.cuda.Stream] = None):
+    """index_device_blocks plus the opt-in Adler-32 per block (0 for a block
+    outside the buffer) -> (digests uint8[n, 20], weak int32[n])."""
+    _require_device(data, "data", torch.uint8)
+    _require_device(offsets, "offsets", torch.int64)
+    _require_device(sizes, "sizes", torch.int32)
+    n = offsets.numel()
+    if sizes.numel() != n:
+        raise ValueError("offsets and sizes differ in length")
+    out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+    weak = torch.empty(n, dtype=torch.int32, device=data.device)
+    if n == 0:
+        return out, weak
+    status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
+    with torch.cuda.device(data.device):
+        check(lib().sf_index_device_blocks_weak(data.data_ptr() if data.numel() else None, data.numel(),
+                                                offsets.data_ptr(), sizes.data_ptr(), n, out.data_ptr(),
+                                                weak.data_ptr(), status.data_ptr() if status is not None else None,
+                                                _stream_ptr(data, stream)),
+              "sf_index_device_blocks_weak")
+    if status is not None and int(status.item()) != 0:
+        raise SfError(SF_ERANGE, "sf_index_device_blocks_weak")
+    return out, weak
 
 
 def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], block_size: int,

@@ -85,3 +85,21 @@ def test_c_matches_python_random():
         _, _, d = oracle.index_fixed(data, bs)
         _, _, want = oracle.py_index_fixed(data, bs)
         assert [bytes(x) for x in d] == want
+
+
+def test_adler_oracle_matches_zlib():
+    # the opt-in weak sum's checker (not a reference path: SURVEY.md 8a row a8)
+    import zlib
+    rng = np.random.default_rng(11)
+    data = oracle.splitmix_bytes(300_000, 77).tobytes()
+    assert oracle.adler32(b"") == zlib.adler32(b"") == 1
+    for n in [1, 63, 64, 65, 4095, 4096, 4097, 5553, 300_000]:
+        assert oracle.adler32(data[:n]) == zlib.adler32(data[:n]), n
+    worst = b"\xff" * (1 << 20)  # largest sums: overflow guard
+    assert oracle.adler32(worst) == zlib.adler32(worst)
+    for _ in range(5):
+        bs = int(rng.integers(1, 70_000))
+        want = [zlib.adler32(data[i:i + bs]) for i in range(0, len(data), bs)]
+        assert oracle.adler_fixed(data, bs).tolist() == want
+    offs, sizes = [0, 17, 1000, 299_990], [0, 5000, 64, 10]
+    assert oracle.adler_blocks(data, offs, sizes).tolist() == [zlib.adler32(data[o:o + s]) for o, s in zip(offs, sizes)]
