@@ -66,6 +66,9 @@ def parse():
                         "~6 launches to ramp its clock from ~1.6 GHz; see DESIGN.md section 4)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--weak", action="store_true",
+                   help="also compute the opt-in fused Adler-32 weak sum per block (not in the reference; "
+                        "configs 2 and 5 only); not the headline")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
@@ -148,6 +151,9 @@ def main():
         flen = shard // cfg["files"]
         files = [(i * flen, flen) for i in range(cfg["files"])]
     fhash = torch.empty((len(files), 20), dtype=torch.uint8, device=dev) if files else None
+    if a.weak and files is not None:
+        raise SystemExit("--weak applies to configs 2 and 5")
+    weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)] if a.weak else None
     gather = distributed and not a.no_gather
     torch.cuda.synchronize()
 
@@ -165,7 +171,9 @@ def main():
             pending[b] = None
         if timed:
             ev[i][0].record(stream)
-        if files is None:
+        if weaks is not None:
+            device.index_device_weak(data, bs, out=digs[b], weak_out=weaks[b], stream=stream)
+        elif files is None:
             device.index_device(data, bs, out=digs[b], stream=stream)
         else:
             device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
@@ -186,7 +194,10 @@ def main():
     # Setup (not a step): clock ramp, untimed, no gather.
     t_ramp = time.perf_counter()
     while time.perf_counter() - t_ramp < a.ramp_s:
-        device.index_device(data, bs, out=digs[0], stream=stream)
+        if weaks is not None:
+            device.index_device_weak(data, bs, out=digs[0], weak_out=weaks[0], stream=stream)
+        else:
+            device.index_device(data, bs, out=digs[0], stream=stream)
         torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i, False)
@@ -244,6 +255,8 @@ def main():
     alg_bytes = nblk * (bs + 20)  # read every byte once + write 20 B/block
     if files is not None:  # + per-file blocks_hash kernel: re-read the digests, write 20 B/file
         alg_bytes += nblk * 20 + len(files) * 20
+    if weaks is not None:  # + 4 B weak sum written per block
+        alg_bytes += nblk * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
@@ -260,7 +273,8 @@ def main():
         cpu_all = cpu_baseline_all_cores(shard, bs, a.cpu_seconds / 4)
 
     line = {
-        "metric": "GiB/s indexed (device-resident), %d KiB blocks" % (bs // 1024),
+        "metric": "GiB/s indexed (device-resident), %d KiB blocks" % (bs // 1024)
+                  + (" + opt-in Adler-32 weak sum" if weaks is not None else ""),
         "value": round(gibs, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -278,7 +292,8 @@ def main():
                                                      "_gather(pipelined)" if gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "sha1_fixed_kernel<128>", "kernel_ms": round(kern_ms, 4),
+                     "kernel": "sha1_fixed_kernel<128%s>" % (", 1, true" if weaks is not None else ""),
+                     "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all,
