@@ -263,7 +263,7 @@ def main():
         with open(a.traffic_file) as f:
             tr = json.load(f)
         key = f"config{a.config}"
-        if key in tr and tr[key].get("shard_bytes") == shard:
+        if key in tr and tr[key].get("shard_bytes") == shard and not a.weak:
             traffic = tr[key]["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
