@@ -66,6 +66,9 @@ def parse():
                         "~6 launches to ramp its clock from ~1.6 GHz; see DESIGN.md section 4)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--c3-mode", default="stream", choices=("stream", "staged"),
+                   help="config 3: 'stream' = batch after batch, each launch also finishing the previous batch's "
+                        "blocks_hash (sf_index_device_batch_chained); 'staged' = one self-contained launch per batch")
     p.add_argument("--weak", action="store_true",
                    help="also compute the opt-in fused Adler-32 weak sum per block (not in the reference; "
                         "configs 2 and 5 only); not the headline")
@@ -154,6 +157,7 @@ def main():
     if a.weak and files is not None:
         raise SystemExit("--weak applies to configs 2 and 5")
     weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)] if a.weak else None
+    bstream = device.BatchStream(len(files), flen, bs, stream=stream) if files and a.c3_mode == "stream" else None
     gather = distributed and not a.no_gather
     torch.cuda.synchronize()
 
@@ -175,6 +179,8 @@ def main():
             device.index_device_weak(data, bs, out=digs[b], weak_out=weaks[b], stream=stream)
         elif files is None:
             device.index_device(data, bs, out=digs[b], stream=stream)
+        elif bstream is not None:
+            bstream.push(data, digs[b], hashes=fhash)
         else:
             device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
                                       stream=stream)
@@ -201,6 +207,8 @@ def main():
         torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i, False)
+    if bstream is not None:
+        bstream.finish(hashes=fhash)
     drain()
     torch.cuda.synchronize()
     if distributed:
@@ -209,6 +217,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i, True)
+    if bstream is not None:  # the last batch's blocks_hash: inside the timed region
+        bstream.finish(hashes=fhash)
     drain()
     torch.cuda.synchronize()
     if distributed:
@@ -232,6 +242,11 @@ def main():
     first = data[:bs].cpu().numpy()
     lastb = data[(nblk - 1) * bs:].cpu().numpy()
     assert bytes(d[0]) == host.sha1(first) and bytes(d[-1]) == host.sha1(lastb), "digest self-check failed"
+    if files is not None:  # the last batch's per-file blocks_hash (device) vs the host SHA-1 of its rows
+        per_file = d.reshape(len(files), -1, 20)
+        fh = fhash.cpu().numpy()
+        for f in (0, len(files) - 1):
+            assert bytes(fh[f]) == host.blocks_hash(per_file[f]), "blocks_hash self-check failed"
 
     if rank != 0:
         if distributed:
@@ -288,11 +303,14 @@ def main():
         "data": "synthetic (splitmix64 bytes generated in HBM, seed 0x5EED0000)",
         "config": {"workload": cfg["workload"], "bytes_per_gpu": shard, "block_size": bs,
                    "total_bytes": total_bytes, "files": cfg["files"], "blocks": nblk * world,
+                   **({"c3_mode": a.c3_mode} if files else {}),
                    "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else a.dist_backend}"
                                                      "_gather(pipelined)" if gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "sha1_fixed_kernel<128%s>" % (", 1, true" if weaks is not None else ""),
+                     "kernel": ("sha1_fixed_chained_kernel<128>" if bstream is not None else
+                                "sha1_staged_kernel<128>" if files else
+                                "sha1_fixed_kernel<128%s>" % (", 1, true" if weaks is not None else "")),
                      "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,

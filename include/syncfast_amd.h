@@ -116,6 +116,21 @@ int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
                           uint64_t *n_blocks, void *stream);
 
+/* Equal-size many-file batches as a stream (BASELINE config 3, batch after
+ * batch, the shape of index_path over a large tree): ONE launch on `stream`
+ * hashes every block of this batch -- n_files files of file_len bytes
+ * (a multiple of block_size) back to back at d_data -- into d_digests
+ * (file-major rows) and, in the same launch, the blocks_hash
+ * (src/index.rs:661-682) of the PREVIOUS batch's prev_files files from its
+ * digest table d_prev_digests (prev_blocks rows per file, a multiple of 4)
+ * into d_prev_hashes (20 B per file).  The previous batch's digests must
+ * come from an earlier launch on the same stream.  n_files = 0 only finishes
+ * the previous batch; d_prev_digests = NULL starts a stream. */
+int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t file_len,
+                                  uint32_t block_size, void *d_digests, const void *d_prev_digests,
+                                  uint32_t prev_files, uint64_t prev_blocks, void *d_prev_hashes,
+                                  void *stream);
+
 /* The signature table as the reference's wire messages, on the device:
  * n_blocks FILE_BLOCK messages, "FILE_BLOCK\n" + 20 digest bytes + "\n" +
  * decimal block size + "\n" (write_message, src/sync/ssh/proto.rs:162-166),

@@ -29,7 +29,7 @@ MAX_BLOCK_SIZE = 32 << 20
 EXPORTED = (
     "sf_version", "sf_strerror", "sf_device_count", "sf_set_device",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
-    "sf_index_device_fixed_weak", "sf_index_device_blocks_weak",
+    "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_index_buffer", "sf_index_file", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
 )
@@ -70,6 +70,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_index_device_blocks.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp]
     L.sf_index_device_fixed_weak.argtypes = [vp, u64, u32, vp, vp, u64, pu64, vp]
     L.sf_index_device_blocks_weak.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp, vp]
+    L.sf_index_device_batch_chained.argtypes = [vp, u32, u64, u32, vp, vp, u32, u64, vp, vp]
     L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp]
     L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]

@@ -429,6 +429,30 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   return rc;
 }
 
+int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t file_len, uint32_t block_size,
+                                  void* d_digests, const void* d_prev_digests, uint32_t prev_files,
+                                  uint64_t prev_blocks, void* d_prev_hashes, void* stream) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (n_files && (file_len == 0 || file_len % block_size)) return SF_EINVAL;
+  const uint64_t total = n_files ? (file_len / block_size) * n_files : 0;
+  const bool chains = d_prev_digests != nullptr && prev_files > 0;
+  // each file's digest run must start 16-B aligned (20 * prev_blocks % 16 == 0)
+  if (chains && (!d_prev_hashes || prev_blocks == 0 || prev_blocks % 4 || prev_blocks * 20 > 0xFFFFFFF0ull))
+    return SF_EINVAL;
+  if (total && (!d_data || !d_digests)) return SF_EINVAL;
+  if (!total && !chains) return SF_OK;
+  hipStream_t s = as_stream(stream);
+  const unsigned chain_wgs = chains ? (unsigned)ceil_div(prev_files, 64 * sf::kWavesPerWG) : 0u;
+  const unsigned grid = chain_wgs + (total ? grid_for_blocks(total) : 0u);
+  hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s,
+                     static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
+                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size),
+                     static_cast<const uint8_t*>(d_prev_digests), prev_files, (uint32_t)(prev_blocks * 20),
+                     static_cast<uint8_t*>(d_prev_hashes), chain_wgs);
+  return hip_err(hipGetLastError());
+}
+
 int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len,
                                void* d_out, uint64_t cap, uint64_t* n_out, void* stream) {
   if (block_size == 0 || block_size > SF_MAX_BLOCK_SIZE) return SF_EINVAL;

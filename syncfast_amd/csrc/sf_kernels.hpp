@@ -297,17 +297,16 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 
 // ---------------------------------------------------------------- kernels
 
-// Fixed tiling: block i = data[i*bs, min((i+1)*bs, len)).
-// WPE = minimum resident waves per SIMD requested from the register
-// allocator (__launch_bounds__ 2nd argument, per EU on gfx950).
-template <int TILE, int WPE = 1, bool WEAK = false>
-__global__ void __launch_bounds__(kThreads, WPE)
-sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                  uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
-  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+// Fixed tiling: block i = data[i*bs, min((i+1)*bs, len)).  One workgroup
+// `group` of it (4 waves x 64 consecutive blocks): the body of
+// sha1_fixed_kernel and of the block part of sha1_fixed_chained_kernel.
+template <int TILE, bool WEAK>
+__device__ __forceinline__ void fixed_group(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs,
+                                            uint64_t nblocks, uint8_t* __restrict__ digests, const PadSchedule pad,
+                                            uint32_t* __restrict__ weak, uint32_t group, uint4* __restrict__ smem) {
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
-  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
+  const uint64_t first = ((uint64_t)group * kWavesPerWG + wid) * 64;
   if (first >= nblocks) return;
   const uint64_t blk = first + lane;
   const bool valid = blk < nblocks;
@@ -333,6 +332,16 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
     st.store(digests + blk * 20);
     if constexpr (WEAK) weak[blk] = wk.fin();
   }
+}
+
+// WPE = minimum resident waves per SIMD requested from the register
+// allocator (__launch_bounds__ 2nd argument, per EU on gfx950).
+template <int TILE, int WPE = 1, bool WEAK = false>
+__global__ void __launch_bounds__(kThreads, WPE)
+sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
+                  uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  fixed_group<TILE, WEAK>(data, len, bs, nblocks, digests, pad, weak, blockIdx.x, smem);
 }
 
 // Stream a 64-B-multiple byte range [lo, hi) of a lane's message through
@@ -417,6 +426,79 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
                   uint8_t* __restrict__ out) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
   chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr);
+}
+
+// Deep-prefetch form of sha1_stream_range for chains that run beside a
+// streaming block launch (their digest loads miss to HBM under load): D
+// chunks (D x 64 B per lane) stay in flight.  nch is wave-uniform (every
+// file of a batch has the same run length); q must be 16-B aligned.
+template <int D>
+__device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restrict__ q, uint32_t nch) {
+  if (nch == 0) return;
+  uint4 buf[D][4];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const uint32_t c = (uint32_t)k < nch ? (uint32_t)k : nch - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)c * 4 + i];
+  }
+  for (uint32_t c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const uint32_t c = c0 + k;
+      if (c < nch) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          w[4 * i + 0] = bswap32(buf[k][i].x);
+          w[4 * i + 1] = bswap32(buf[k][i].y);
+          w[4 * i + 2] = bswap32(buf[k][i].z);
+          w[4 * i + 3] = bswap32(buf[k][i].w);
+        }
+        const uint32_t nx = c + D < nch ? c + D : nch - 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)nx * 4 + i];
+        st.compress(w);
+      }
+    }
+  }
+}
+
+// Equal-size many-file batches as a stream (BASELINE configs[2], batch after
+// batch): ONE launch hashes every block of batch i (fixed_group, in
+// workgroups [chain_wgs, grid)) and, in workgroups [0, chain_wgs), the
+// per-file blocks_hash (src/index.rs:661-682) of batch i-1: one lane per
+// file over its run of run_len digest bytes.  Batch i-1's digest table was
+// completed by the previous launch on the same stream, so no workgroup of
+// this launch waits on another; the chains (640 compressions per 8 MiB file,
+// single-lane latency bound) hide behind the block work instead of trailing
+// it.
+template <int TILE>
+__global__ void __launch_bounds__(kThreads, 1)
+sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
+                          uint8_t* __restrict__ digests, const PadSchedule pad, const uint8_t* __restrict__ prev,
+                          uint32_t prev_files, uint32_t run_len, uint8_t* __restrict__ prev_hashes,
+                          uint32_t chain_wgs) {
+  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  if (blockIdx.x < chain_wgs) {
+    __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + (threadIdx.x & 63);
+    if (f >= prev_files) return;
+    const uint8_t* p = prev + (uint64_t)f * run_len;
+    Sha1 st;
+    st.init();
+    sha1_stream_deep<4>(st, reinterpret_cast<const uint4*>(p), run_len / 64);
+    const uint32_t nch = n_chunks(run_len);
+    for (uint32_t c = run_len / 64; c < nch; ++c) {
+      uint32_t w[16];
+      build_tail_chunk(w, p, run_len, c, nch);
+      st.compress(w);
+    }
+    st.store(prev_hashes + (uint64_t)f * 20);
+    return;
+  }
+  fixed_group<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, blockIdx.x - chain_wgs, smem);
 }
 
 #ifdef SF_TUNING

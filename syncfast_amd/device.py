@@ -24,7 +24,7 @@ from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
 
 __all__ = [
     "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
-    "index_device_weak", "index_device_blocks_weak",
+    "index_device_weak", "index_device_blocks_weak", "BatchStream",
     "fill_splitmix", "splitmix_tensor",
 ]
 
@@ -187,6 +187,58 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
                                           first.ctypes.data, ctypes.byref(nb), _stream_ptr(data, stream)),
               "sf_index_device_batch")
     return dig, first.astype(np.int64), fh
+
+
+class BatchStream:
+    """Equal-size many-file batches streamed through the device
+    (sf_index_device_batch_chained): push() hashes one batch's blocks and, in
+    the SAME launch, the previous batch's per-file blocks_hash; finish()
+    completes the last batch.  Every batch is n_files files of file_len
+    bytes back to back in one uint8 HBM tensor.
+
+    push(data, digests_out) -> the hashes tensor of the PREVIOUS batch (filled
+    by this launch; None on the first push).  finish() -> the last batch's.
+    A batch's digest table must stay alive until the next push/finish."""
+
+    def __init__(self, n_files: int, file_len: int, block_size: int, stream: Optional[torch.cuda.Stream] = None):
+        if file_len <= 0 or file_len % block_size:
+            raise ValueError("file_len must be a positive multiple of block_size")
+        self.n_files, self.file_len, self.block_size = n_files, file_len, block_size
+        self.nbf = file_len // block_size
+        self.stream = stream
+        self._prev = None  # previous batch's digest table
+
+    def _launch(self, data, digests, hashes):
+        prev = self._prev
+        ref = data if data is not None else prev
+        with torch.cuda.device(ref.device):
+            check(lib().sf_index_device_batch_chained(
+                data.data_ptr() if data is not None else None, self.n_files if data is not None else 0,
+                self.file_len, self.block_size, digests.data_ptr() if digests is not None else None,
+                prev.data_ptr() if prev is not None else None, self.n_files if prev is not None else 0,
+                self.nbf, hashes.data_ptr() if hashes is not None else None, _stream_ptr(ref, self.stream)),
+                "sf_index_device_batch_chained")
+
+    def push(self, data: torch.Tensor, digests: torch.Tensor, hashes: Optional[torch.Tensor] = None):
+        _require_device(data, "data", torch.uint8)
+        _require_device(digests, "digests", torch.uint8)
+        if data.numel() != self.n_files * self.file_len or digests.numel() < 20 * self.n_files * self.nbf:
+            raise ValueError("batch or digest table has the wrong size")
+        if self._prev is not None and hashes is None:
+            hashes = torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device)
+        self._launch(data, digests, hashes if self._prev is not None else None)
+        out = hashes if self._prev is not None else None
+        self._prev = digests
+        return out
+
+    def finish(self, hashes: Optional[torch.Tensor] = None):
+        if self._prev is None:
+            return None
+        if hashes is None:
+            hashes = torch.empty((self.n_files, 20), dtype=torch.uint8, device=self._prev.device)
+        self._launch(None, None, hashes)
+        self._prev = None
+        return hashes
 
 
 def fill_splitmix(out: torch.Tensor, seed: int, start: int = 0,
