@@ -157,11 +157,11 @@ def main():
     if a.weak and files is not None:
         raise SystemExit("--weak applies to configs 2 and 5")
     weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)] if a.weak else None
-    bstream = device.BatchStream(len(files), flen, bs, stream=stream) if files and a.c3_mode == "stream" else None
     gather = distributed and not a.no_gather
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    bstream = device.BatchStream(len(files), flen, bs, stream=stream) if files and a.c3_mode == "stream" else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     pending = [None, None]
     last_table = [None]
