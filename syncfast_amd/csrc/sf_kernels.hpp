@@ -473,6 +473,9 @@ __device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restri
 // this launch waits on another; the chains (640 compressions per 8 MiB file,
 // single-lane latency bound) hide behind the block work instead of trailing
 // it.
+#ifndef SF_CHAIN_DEPTH
+#define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
+#endif
 template <int TILE>
 __global__ void __launch_bounds__(kThreads, 1)
 sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
@@ -488,7 +491,7 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
     const uint8_t* p = prev + (uint64_t)f * run_len;
     Sha1 st;
     st.init();
-    sha1_stream_deep<4>(st, reinterpret_cast<const uint4*>(p), run_len / 64);
+    sha1_stream_deep<SF_CHAIN_DEPTH>(st, reinterpret_cast<const uint4*>(p), run_len / 64);
     const uint32_t nch = n_chunks(run_len);
     for (uint32_t c = run_len / 64; c < nch; ++c) {
       uint32_t w[16];
