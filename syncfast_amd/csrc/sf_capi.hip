@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <stdint.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <stdlib.h>
 #include <string.h>
@@ -563,6 +564,33 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   if (n_out) *n_out = nb;
   if (nb > cap) { close(fd); return SF_ENOSPC; }
   if (nb && !out) { close(fd); return SF_EINVAL; }
+  // A large file already in the page cache: map it and page-lock the mapping
+  // in place (hipHostRegister), so the DMA engine reads the page-cache pages
+  // directly -- no pread copy (the in-place path of sf_index_buffer).  A file
+  // that is mostly not resident keeps the pread pipeline, which overlaps the
+  // disk reads with the device.  SF_NO_MMAP=1 forces pread (A/B knob).
+  const char* nomm = getenv("SF_NO_MMAP");
+  if (len >= (64ull << 20) && !(nomm && atoi(nomm))) {
+    void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
+    if (m != MAP_FAILED) {
+      const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+      std::vector<unsigned char> res(ceil_div(len, pg));
+      uint64_t resident = 0;
+      if (mincore(m, len, res.data()) == 0)
+        for (unsigned char r : res) resident += r & 1u;
+      if (resident * 10 >= res.size() * 9 &&
+          hipHostRegister(m, len, hipHostRegisterReadOnly) == hipSuccess) {
+        rc = index_registered(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out);
+        (void)hipHostUnregister(m);
+        munmap(m, len);
+        close(fd);
+        if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
+        return rc;
+      }
+      (void)hipGetLastError();
+      munmap(m, len);
+    }
+  }
   // Each stage is read by several threads in parallel (one pread stream per
   // slice): one thread copies from the page cache at ~16 GB/s, below PCIe.
   const unsigned nthreads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));

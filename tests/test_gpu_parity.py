@@ -186,6 +186,25 @@ def test_index_file_end_to_end(gpu):
     assert bh == oracle.blocks_hash(want)
 
 
+@pytest.mark.parametrize("no_mmap", ["0", "1"])
+def test_index_file_large_both_routes(gpu, no_mmap, monkeypatch):
+    # >= 64 MiB and in the page cache (just written): the mmap + hostRegister
+    # route; SF_NO_MMAP=1 forces the pread pipeline.  Same rows either way.
+    monkeypatch.setenv("SF_NO_MMAP", no_mmap)
+    data = oracle.splitmix_bytes((96 << 20) + 4093, 95)
+    with tempfile.NamedTemporaryFile(delete=False) as f:
+        f.write(data.tobytes())
+        path = f.name
+    try:
+        rows, bh = host.index_file(path, 4096)
+    finally:
+        os.unlink(path)
+    offs, sizes, want = oracle.index_fixed(data, 4096)
+    assert np.array_equal(rows["sha1"], want)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    assert bh == oracle.blocks_hash(want)
+
+
 def test_block_digest_independent_of_neighbours(gpu):
     # the same block bytes at different positions / in different waves give
     # the same digest (no cross-lane leakage through the LDS tile)
