@@ -148,7 +148,8 @@ def main():
     device.fill_splitmix(data, SEED, start)
     # Two digest tables: step i writes table i%2 while the gather of step
     # i-1's table is still in flight (RCCL runs on its own stream).
-    digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=dev) for _ in range(2)]
+    nbuf = 3 if (cfg["files"] > 1 and a.c3_mode == "stream") else 2  # split chains read batch i-2's table
+    digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     files = None
     if cfg["files"] > 1:
         flen = shard // cfg["files"]
@@ -163,11 +164,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     bstream = device.BatchStream(len(files), flen, bs, stream=stream) if files and a.c3_mode == "stream" else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    pending = [None, None]
+    pending = [None] * nbuf
     last_table = [None]
+    last_hashes = [None]  # batch stream: blocks_hash of the latest finished batch
 
     def step(i, timed):
-        b = i % 2
+        b = i % nbuf
         if pending[b] is not None:  # the gather that reads digs[b] must be done
             work, finish = pending[b]
             work.wait()
@@ -180,7 +182,9 @@ def main():
         elif files is None:
             device.index_device(data, bs, out=digs[b], stream=stream)
         elif bstream is not None:
-            bstream.push(data, digs[b], hashes=fhash)
+            h = bstream.push(data, digs[b])
+            if h is not None:
+                last_hashes[0] = h
         else:
             device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
                                       stream=stream)
@@ -190,7 +194,7 @@ def main():
             pending[b] = gather_digests(digs[b], total, bs, async_op=True)
 
     def drain():
-        for b in range(2):
+        for b in range(nbuf):
             if pending[b] is not None:
                 work, finish = pending[b]
                 work.wait()
@@ -208,7 +212,7 @@ def main():
     for i in range(a.warmup):
         step(i, False)
     if bstream is not None:
-        bstream.finish(hashes=fhash)
+        bstream.finish()
     drain()
     torch.cuda.synchronize()
     if distributed:
@@ -217,8 +221,10 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i, True)
-    if bstream is not None:  # the last batch's blocks_hash: inside the timed region
-        bstream.finish(hashes=fhash)
+    if bstream is not None:  # the last batches' blocks_hash: inside the timed region
+        fin = bstream.finish()
+        if fin:
+            last_hashes[0] = fin[-1]
     drain()
     torch.cuda.synchronize()
     if distributed:
@@ -234,7 +240,7 @@ def main():
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
     t = float(elapsed.item())
     kern_ms = float(kt.item())
-    dig = digs[(a.steps - 1) % 2]
+    dig = digs[(a.steps - 1) % nbuf]
     gathered = last_table[0]() if last_table[0] is not None else None
 
     # Self-check (product host SHA-1): first and last block of this shard.
@@ -244,7 +250,7 @@ def main():
     assert bytes(d[0]) == host.sha1(first) and bytes(d[-1]) == host.sha1(lastb), "digest self-check failed"
     if files is not None:  # the last batch's per-file blocks_hash (device) vs the host SHA-1 of its rows
         per_file = d.reshape(len(files), -1, 20)
-        fh = fhash.cpu().numpy()
+        fh = (last_hashes[0] if bstream is not None else fhash).cpu().numpy()
         for f in (0, len(files) - 1):
             assert bytes(fh[f]) == host.blocks_hash(per_file[f]), "blocks_hash self-check failed"
 

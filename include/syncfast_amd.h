@@ -116,20 +116,31 @@ int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
                           uint64_t *n_blocks, void *stream);
 
+/* Per-file blocks_hash (src/index.rs:661-682) of a batch of equal-size files
+ * already hashed into d_digests (n_files files x blocks rows, blocks a
+ * multiple of 4): part 0 = whole chains -> d_hashes (20 B per file);
+ * part 1 = first half of every chain -> d_state (20 B per file);
+ * part 2 = second half, resumed from d_state -> d_hashes. */
+typedef struct sf_chain_job {
+    const void *d_digests;
+    uint32_t n_files;
+    uint32_t part;
+    uint64_t blocks;
+    void *d_state;
+    void *d_hashes;
+} sf_chain_job;
+
 /* Equal-size many-file batches as a stream (BASELINE config 3, batch after
  * batch, the shape of index_path over a large tree): ONE launch on `stream`
- * hashes every block of this batch -- n_files files of file_len bytes
- * (a multiple of block_size) back to back at d_data -- into d_digests
- * (file-major rows) and, in the same launch, the blocks_hash
- * (src/index.rs:661-682) of the PREVIOUS batch's prev_files files from its
- * digest table d_prev_digests (prev_blocks rows per file, a multiple of 4)
- * into d_prev_hashes (20 B per file).  The previous batch's digests must
- * come from an earlier launch on the same stream.  n_files = 0 only finishes
- * the previous batch; d_prev_digests = NULL starts a stream. */
+ * hashes every block of this batch -- n_files files of file_len bytes (a
+ * multiple of block_size) back to back at d_data -- into d_digests
+ * (file-major rows) and, in the same launch, up to two chain jobs of EARLIER
+ * batches (digests and states written by earlier launches on the same
+ * stream), so their blocks_hash latency hides behind this batch's blocks.
+ * n_files = 0 runs only the jobs. */
 int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t file_len,
-                                  uint32_t block_size, void *d_digests, const void *d_prev_digests,
-                                  uint32_t prev_files, uint64_t prev_blocks, void *d_prev_hashes,
-                                  void *stream);
+                                  uint32_t block_size, void *d_digests, const sf_chain_job *jobs,
+                                  uint32_t n_jobs, void *stream);
 
 /* The signature table as the reference's wire messages, on the device:
  * n_blocks FILE_BLOCK messages, "FILE_BLOCK\n" + 20 digest bytes + "\n" +

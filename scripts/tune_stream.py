@@ -1,7 +1,7 @@
-"""Where the time of the chained batch-stream launch goes (config 3 shape):
-plain fixed kernel over the same 8 GiB, the chained kernel with and without
-the previous batch's chains, and the chains alone (finish on an idle GPU).
-Interleaved rounds in one process; medians in ms."""
+"""Config 3 as a stream of batches: per-batch time of the plain fixed kernel
+(no blocks_hash, reference point) vs the batch stream with whole chains and
+with split chains (blocks_hash of every file included).  Each stream round =
+10 pushes + finish; interleaved rounds in one process; medians in ms/batch."""
 import os
 import statistics
 import sys
@@ -11,51 +11,42 @@ import torch  # noqa: E402
 
 from syncfast_amd import device  # noqa: E402
 
-GiB = 1 << 30
-
 
 def main():
     nf, flen, bs = 1024, 8 << 20, 4096
     data = device.splitmix_tensor(nf * flen, 0x5EED0000)
     n = nf * flen // bs
-    d = [torch.empty((n, 20), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    fh = torch.empty((nf, 20), dtype=torch.uint8, device="cuda")
+    d = [torch.empty((n, 20), dtype=torch.uint8, device="cuda") for _ in range(3)]
     s = torch.cuda.current_stream()
+    K = 10
 
     def plain():
-        device.index_device(data, bs, out=d[0])
+        for i in range(K):
+            device.index_device(data, bs, out=d[i % 3])
 
-    st = device.BatchStream(nf, flen, bs)
-    st.push(data, d[1])  # d[1] = "previous batch" from here on
+    def stream(split):
+        def run():
+            st = device.BatchStream(nf, flen, bs, split=split)
+            for i in range(K):
+                st.push(data, d[i % 3])
+            st.finish()
+        return run
 
-    def chained():
-        st._prev = d[1]
-        st._launch(data, d[0], fh)
-
-    def chained_nochain():
-        st._prev = None
-        st._launch(data, d[0], None)
-
-    def chains_only():
-        st._prev = d[1]
-        st._launch(None, None, fh)
-
-    cases = [("plain fixed", plain), ("chained (blocks + prev chains)", chained),
-             ("chained, no chains", chained_nochain), ("chains only", chains_only)]
-    for _ in range(30):
+    cases = [("plain fixed (no blocks_hash)", plain), ("stream, whole chains", stream(False)),
+             ("stream, split chains", stream(True))]
+    for _ in range(3):
         plain()
     times = {k: [] for k, _ in cases}
-    for _ in range(int(os.environ.get("ROUNDS", "8"))):
+    for _ in range(int(os.environ.get("ROUNDS", "6"))):
         for name, fn in cases:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            for _ in range(5):
-                fn()
+            fn()
             e1.record(s)
             torch.cuda.synchronize()
-            times[name].append(e0.elapsed_time(e1) / 5)
+            times[name].append(e0.elapsed_time(e1) / K)
     for name, _ in cases:
-        print(f"{name}: median {statistics.median(times[name]):.4f} ms  min {min(times[name]):.4f}", flush=True)
+        print(f"{name}: median {statistics.median(times[name]):.4f} ms/batch  min {min(times[name]):.4f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -50,6 +50,12 @@ class BlockSig(ctypes.Structure):
                 ("sha1", ctypes.c_uint8 * 20)]
 
 
+class ChainJob(ctypes.Structure):
+    """sf_chain_job: one blocks_hash chain job of an earlier batch."""
+    _fields_ = [("d_digests", ctypes.c_void_p), ("n_files", ctypes.c_uint32), ("part", ctypes.c_uint32),
+                ("blocks", ctypes.c_uint64), ("d_state", ctypes.c_void_p), ("d_hashes", ctypes.c_void_p)]
+
+
 class FileDesc(ctypes.Structure):
     _fields_ = [("offset", ctypes.c_uint64), ("len", ctypes.c_uint64)]
 
@@ -70,7 +76,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_index_device_blocks.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp]
     L.sf_index_device_fixed_weak.argtypes = [vp, u64, u32, vp, vp, u64, pu64, vp]
     L.sf_index_device_blocks_weak.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp, vp]
-    L.sf_index_device_batch_chained.argtypes = [vp, u32, u64, u32, vp, vp, u32, u64, vp, vp]
+    L.sf_index_device_batch_chained.argtypes = [vp, u32, u64, u32, vp, ctypes.POINTER(ChainJob), u32, vp]
     L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp]
     L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]

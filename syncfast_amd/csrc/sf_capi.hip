@@ -431,26 +431,37 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
 }
 
 int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t file_len, uint32_t block_size,
-                                  void* d_digests, const void* d_prev_digests, uint32_t prev_files,
-                                  uint64_t prev_blocks, void* d_prev_hashes, void* stream) {
+                                  void* d_digests, const sf_chain_job* jobs, uint32_t n_jobs, void* stream) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
   if (n_files && (file_len == 0 || file_len % block_size)) return SF_EINVAL;
+  if (n_jobs > 2 || (n_jobs && !jobs)) return SF_EINVAL;
   const uint64_t total = n_files ? (file_len / block_size) * n_files : 0;
-  const bool chains = d_prev_digests != nullptr && prev_files > 0;
-  // each file's digest run must start 16-B aligned (20 * prev_blocks % 16 == 0)
-  if (chains && (!d_prev_hashes || prev_blocks == 0 || prev_blocks % 4 || prev_blocks * 20 > 0xFFFFFFF0ull))
-    return SF_EINVAL;
   if (total && (!d_data || !d_digests)) return SF_EINVAL;
-  if (!total && !chains) return SF_OK;
-  hipStream_t s = as_stream(stream);
-  const unsigned chain_wgs = chains ? (unsigned)ceil_div(prev_files, 64 * sf::kWavesPerWG) : 0u;
-  const unsigned grid = chain_wgs + (total ? grid_for_blocks(total) : 0u);
-  hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s,
+  sf::ChainJob cj[2] = {};
+  for (uint32_t k = 0; k < n_jobs; k++) {
+    const sf_chain_job& j = jobs[k];
+    if (!j.n_files) continue;
+    // each file's digest run must start 16-B aligned (20 * blocks % 16 == 0)
+    if (!j.d_digests || j.blocks == 0 || j.blocks % 4 || j.blocks * 20 > 0xFFFFFFF0ull || j.part > 2 ||
+        (j.part != 0 && !j.d_state) || (j.part != 1 && !j.d_hashes))
+      return SF_EINVAL;
+    const uint32_t run_len = (uint32_t)(j.blocks * 20), data_ch = run_len / 64, half = data_ch / 2;
+    cj[k].runs = static_cast<const uint8_t*>(j.d_digests);
+    cj[k].state = static_cast<uint8_t*>(j.d_state);
+    cj[k].hashes = static_cast<uint8_t*>(j.d_hashes);
+    cj[k].files = j.n_files;
+    cj[k].run_len = run_len;
+    cj[k].lo = j.part == 2 ? half : 0;
+    cj[k].hi = j.part == 1 ? half : data_ch;
+    cj[k].part = j.part;
+    cj[k].wgs = (uint32_t)ceil_div(j.n_files, 64 * sf::kWavesPerWG);
+  }
+  const unsigned grid = cj[0].wgs + cj[1].wgs + (total ? grid_for_blocks(total) : 0u);
+  if (grid == 0) return SF_OK;
+  hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),
                      static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
-                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size),
-                     static_cast<const uint8_t*>(d_prev_digests), prev_files, (uint32_t)(prev_blocks * 20),
-                     static_cast<uint8_t*>(d_prev_hashes), chain_wgs);
+                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1]);
   return hip_err(hipGetLastError());
 }
 

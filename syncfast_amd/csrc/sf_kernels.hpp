@@ -464,44 +464,75 @@ __device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restri
   }
 }
 
-// Equal-size many-file batches as a stream (BASELINE configs[2], batch after
-// batch): ONE launch hashes every block of batch i (fixed_group, in
-// workgroups [chain_wgs, grid)) and, in workgroups [0, chain_wgs), the
-// per-file blocks_hash (src/index.rs:661-682) of batch i-1: one lane per
-// file over its run of run_len digest bytes.  Batch i-1's digest table was
-// completed by the previous launch on the same stream, so no workgroup of
-// this launch waits on another; the chains (640 compressions per 8 MiB file,
-// single-lane latency bound) hide behind the block work instead of trailing
-// it.
+// One per-file blocks_hash chain job (src/index.rs:661-682) of a batch of
+// equal-size files: one lane per file over its run of run_len digest bytes,
+// data chunks [lo, hi) (64-B units) of the run.  part 0 = the whole chain;
+// part 1 = chunks [0, hi), the 5-word SHA-1 state saved to state[f]; part 2
+// = resume from state[f], chunks [lo, end) + the padding chunk(s), hash to
+// hashes[f].
+struct ChainJob {
+  const uint8_t* runs;
+  uint8_t* state;
+  uint8_t* hashes;
+  uint32_t files, run_len, lo, hi, part, wgs;
+};
+
 #ifndef SF_CHAIN_DEPTH
 #define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
 #endif
+__device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t g) {
+  __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t f = (g * kWavesPerWG + wid) * 64 + (threadIdx.x & 63);
+  if (f >= j.files) return;
+  const uint8_t* p = j.runs + (uint64_t)f * j.run_len;
+  uint32_t* sv = reinterpret_cast<uint32_t*>(j.state + (uint64_t)f * 20);
+  Sha1 st;
+  if (j.part == 2) {
+    st.h0 = sv[0]; st.h1 = sv[1]; st.h2 = sv[2]; st.h3 = sv[3]; st.h4 = sv[4];
+  } else {
+    st.init();
+  }
+  sha1_stream_deep<SF_CHAIN_DEPTH>(st, reinterpret_cast<const uint4*>(p + (uint64_t)j.lo * 64), j.hi - j.lo);
+  if (j.part == 1) {
+    sv[0] = st.h0; sv[1] = st.h1; sv[2] = st.h2; sv[3] = st.h3; sv[4] = st.h4;
+    return;
+  }
+  const uint32_t nch = n_chunks(j.run_len);
+  for (uint32_t c = j.run_len / 64; c < nch; ++c) {
+    uint32_t w[16];
+    build_tail_chunk(w, p, j.run_len, c, nch);
+    st.compress(w);
+  }
+  st.store(j.hashes + (uint64_t)f * 20);
+}
+
+// Equal-size many-file batches as a stream (BASELINE configs[2], batch after
+// batch): ONE launch hashes every block of batch i (fixed_group) and, in its
+// first workgroups, up to two chain jobs of earlier batches (j0 then j1):
+// with split chains, the second half of batch i-2's and the first half of
+// batch i-1's.  Their digest tables and saved states were completed by
+// earlier launches on the same stream, so no workgroup of this launch waits
+// on another.  Halving each chain halves the latency it needs to hide: a
+// chain lane beside the block waves runs ~3x slower than alone.
 template <int TILE>
 __global__ void __launch_bounds__(kThreads, 1)
 sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                          uint8_t* __restrict__ digests, const PadSchedule pad, const uint8_t* __restrict__ prev,
-                          uint32_t prev_files, uint32_t run_len, uint8_t* __restrict__ prev_hashes,
-                          uint32_t chain_wgs) {
+                          uint8_t* __restrict__ digests, const PadSchedule pad, const ChainJob j0,
+                          const ChainJob j1) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  if (blockIdx.x < chain_wgs) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + (threadIdx.x & 63);
-    if (f >= prev_files) return;
-    const uint8_t* p = prev + (uint64_t)f * run_len;
-    Sha1 st;
-    st.init();
-    sha1_stream_deep<SF_CHAIN_DEPTH>(st, reinterpret_cast<const uint4*>(p), run_len / 64);
-    const uint32_t nch = n_chunks(run_len);
-    for (uint32_t c = run_len / 64; c < nch; ++c) {
-      uint32_t w[16];
-      build_tail_chunk(w, p, run_len, c, nch);
-      st.compress(w);
-    }
-    st.store(prev_hashes + (uint64_t)f * 20);
+  uint32_t g = blockIdx.x;
+  if (g < j0.wgs) {
+    chain_job(j0, g);
     return;
   }
-  fixed_group<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, blockIdx.x - chain_wgs, smem);
+  g -= j0.wgs;
+  if (g < j1.wgs) {
+    chain_job(j1, g);
+    return;
+  }
+  g -= j1.wgs;
+  fixed_group<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, g, smem);
 }
 
 #ifdef SF_TUNING

@@ -191,54 +191,88 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
 
 class BatchStream:
     """Equal-size many-file batches streamed through the device
-    (sf_index_device_batch_chained): push() hashes one batch's blocks and, in
-    the SAME launch, the previous batch's per-file blocks_hash; finish()
-    completes the last batch.  Every batch is n_files files of file_len
-    bytes back to back in one uint8 HBM tensor.
+    (sf_index_device_batch_chained).  Every batch is n_files files of
+    file_len bytes back to back in one uint8 HBM tensor.
 
-    push(data, digests_out) -> the hashes tensor of the PREVIOUS batch (filled
-    by this launch; None on the first push).  finish() -> the last batch's.
-    A batch's digest table must stay alive until the next push/finish."""
+    push(data, digests) hashes the batch's blocks into `digests` and, in the
+    SAME launch, runs the per-file blocks_hash chains of earlier batches:
+    with split=True (default) the second half of batch i-2's chains and the
+    first half of batch i-1's, so a chain needs only half the latency cover.
+    push() returns the blocks_hash tensor (uint8[n_files, 20]) of the batch
+    whose chains this launch completes (i-2 split, i-1 unsplit), or None;
+    finish() returns the remaining ones in batch order.  A batch's digest
+    table must stay alive until its hashes have been returned."""
 
-    def __init__(self, n_files: int, file_len: int, block_size: int, stream: Optional[torch.cuda.Stream] = None):
+    def __init__(self, n_files: int, file_len: int, block_size: int, stream: Optional[torch.cuda.Stream] = None,
+                 split: bool = True):
         if file_len <= 0 or file_len % block_size:
             raise ValueError("file_len must be a positive multiple of block_size")
         self.n_files, self.file_len, self.block_size = n_files, file_len, block_size
         self.nbf = file_len // block_size
+        self.split = split and (self.nbf * 20) // 64 >= 2
         self.stream = stream
-        self._prev = None  # previous batch's digest table
+        self._b = None  # (digests, hashes): batch waiting for its first half / whole chain
+        self._a = None  # (digests, hashes, state): batch waiting for its second half
+        self._states = None
 
-    def _launch(self, data, digests, hashes):
-        prev = self._prev
-        ref = data if data is not None else prev
+    def _job(self, part, entry, state=None):
+        from ._lib import ChainJob
+        d, h = entry[0], entry[1]
+        return ChainJob(d.data_ptr(), self.n_files, part, self.nbf, state.data_ptr() if state is not None else None,
+                        h.data_ptr() if part != 1 else None)
+
+    def _launch(self, data, digests, jobs, ref):
+        from ._lib import ChainJob
+        arr = (ChainJob * max(len(jobs), 1))(*jobs)
         with torch.cuda.device(ref.device):
             check(lib().sf_index_device_batch_chained(
                 data.data_ptr() if data is not None else None, self.n_files if data is not None else 0,
                 self.file_len, self.block_size, digests.data_ptr() if digests is not None else None,
-                prev.data_ptr() if prev is not None else None, self.n_files if prev is not None else 0,
-                self.nbf, hashes.data_ptr() if hashes is not None else None, _stream_ptr(ref, self.stream)),
+                arr, len(jobs), _stream_ptr(ref, self.stream)),
                 "sf_index_device_batch_chained")
 
-    def push(self, data: torch.Tensor, digests: torch.Tensor, hashes: Optional[torch.Tensor] = None):
+    def _step_jobs(self):
+        """Chain jobs for the next launch; advances the pipeline state."""
+        jobs, done = [], None
+        if self.split:
+            if self._a is not None:
+                jobs.append(self._job(2, self._a, self._a[2]))
+                done = self._a[1]
+                self._a = None
+            if self._b is not None:
+                if self._states is None:
+                    dev = self._b[0].device
+                    self._states = [torch.empty((self.n_files, 20), dtype=torch.uint8, device=dev) for _ in range(2)]
+                st = self._states[0]
+                self._states.reverse()  # the next first half writes the other state buffer
+                jobs.append(self._job(1, self._b, st))
+                self._a = (self._b[0], self._b[1], st)
+                self._b = None
+        elif self._b is not None:
+            jobs.append(self._job(0, self._b))
+            done = self._b[1]
+            self._b = None
+        return jobs, done
+
+    def push(self, data: torch.Tensor, digests: torch.Tensor):
         _require_device(data, "data", torch.uint8)
         _require_device(digests, "digests", torch.uint8)
         if data.numel() != self.n_files * self.file_len or digests.numel() < 20 * self.n_files * self.nbf:
             raise ValueError("batch or digest table has the wrong size")
-        if self._prev is not None and hashes is None:
-            hashes = torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device)
-        self._launch(data, digests, hashes if self._prev is not None else None)
-        out = hashes if self._prev is not None else None
-        self._prev = digests
-        return out
+        jobs, done = self._step_jobs()
+        self._launch(data, digests, jobs, data)
+        self._b = (digests, torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device))
+        return done
 
-    def finish(self, hashes: Optional[torch.Tensor] = None):
-        if self._prev is None:
-            return None
-        if hashes is None:
-            hashes = torch.empty((self.n_files, 20), dtype=torch.uint8, device=self._prev.device)
-        self._launch(None, None, hashes)
-        self._prev = None
-        return hashes
+    def finish(self):
+        out = []
+        while self._a is not None or self._b is not None:
+            ref = (self._a or self._b)[0]
+            jobs, done = self._step_jobs()
+            self._launch(None, None, jobs, ref)
+            if done is not None:
+                out.append(done)
+        return out
 
 
 def fill_splitmix(out: torch.Tensor, seed: int, start: int = 0,

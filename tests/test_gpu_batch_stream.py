@@ -17,19 +17,22 @@ def _batch(nf, flen, seed, dev):
     return host, torch.from_numpy(host).to(dev)
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("nf,flen,bs", [(64, 4096 * 16, 4096), (300, 4096 * 8, 4096), (5, 65536 * 4, 65536),
                                          (70, 1000 * 4, 1000)])
-def test_stream_every_digest_and_hash(gpu, nf, flen, bs):
-    st = device.BatchStream(nf, flen, bs)
+def test_stream_every_digest_and_hash(gpu, nf, flen, bs, split):
+    st = device.BatchStream(nf, flen, bs, split=split)
     hosts, digs, hashes = [], [], []
-    for k in range(3):
+    for k in range(4):
         host, t = _batch(nf, flen, 0x5EED0000 + 1000 * k, gpu)
         d = torch.empty((nf * flen // bs, 20), dtype=torch.uint8, device=gpu)
-        hashes.append(st.push(t, d))
+        h = st.push(t, d)
+        if h is not None:
+            hashes.append(h)
         hosts.append(host)
         digs.append(d)
-    hashes = hashes[1:] + [st.finish()]
-    assert st.finish() is None
+    hashes += st.finish()
+    assert st.finish() == [] and len(hashes) == 4
     for host, d, h in zip(hosts, digs, hashes):
         want = np.concatenate([oracle.index_fixed(host[i * flen:(i + 1) * flen], bs)[2] for i in range(nf)])
         assert np.array_equal(d.cpu().numpy(), want)
@@ -45,4 +48,4 @@ def test_stream_rejects_unaligned_runs(gpu):
     d = torch.empty((nf * 6, 20), dtype=torch.uint8, device=gpu)
     st.push(t, d)
     with pytest.raises(SfError):
-        st.push(t, torch.empty_like(d))
+        st.push(t, torch.empty_like(d))  # its launch would chain the first batch
