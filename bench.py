@@ -12,8 +12,9 @@ file is N x 8 GiB, each rank holds its contiguous 8 GiB shard (weak scaling,
 the shard layout of configs[3]) and a step also gathers every shard's digest
 table to rank 0 over RCCL (the exchange the single-file blocks_hash needs).
 
-Also: --config 3 (1024 x 8 MiB files, per-file blocks_hash on device) and
---config 5 (32 GiB, 64 KiB blocks).
+Also: --config 3 (1024 x 8 MiB files, per-file blocks_hash on device),
+--config 4 (32 GiB shard per GPU of one 256 GiB file at 8 GPUs, RCCL gather
+of the 1.25 GiB table) and --config 5 (32 GiB, 64 KiB blocks).
 
 Rank 0 prints ONE JSON line (contract in the task statement), with:
   roofline      -- the SHA-1 kernel's algorithmic bytes / its average launch
@@ -48,6 +49,9 @@ CONFIGS = {
             bytes=8 * GiB, block=4096, files=1),
     3: dict(workload="index 1024 x 8 MiB synthetic files, 4 KiB blocks (BASELINE configs[2])",
             bytes=1024 * 8 * (1 << 20), block=4096, files=1024),
+    4: dict(workload="index one 256 GiB synthetic file, 4 KiB blocks, 32 GiB contiguous shard per GPU "
+                     "(BASELINE configs[3] at --gpus 8; N x 32 GiB at --gpus N)",
+            bytes=32 * GiB, block=4096, files=1),
     5: dict(workload="index one 32 GiB synthetic file, 64 KiB blocks (BASELINE configs[4])",
             bytes=32 * GiB, block=65536, files=1),
 }

@@ -64,3 +64,28 @@ def test_config5_32gib_64k_properties(gpu):
     h1 = device.index_device(data[:half], bs)
     h2 = device.index_device(data[half:], bs)
     assert host.blocks_hash(torch.cat([h1, h2]).cpu().numpy()) == host.blocks_hash(dig)
+
+
+@pytest.mark.parametrize("mode", ["stream", "staged"])
+def test_config3_1024x8mib_every_digest_and_blocks_hash(gpu, mode):
+    # configs[2] at full size: 1024 files x 8 MiB, every digest and every
+    # file's blocks_hash vs the multi-threaded C oracle
+    nf, flen, bs = 1024, 8 << 20, 4096
+    data = device.splitmix_tensor(nf * flen, 0x5EED0002, gpu)
+    if mode == "stream":
+        st = device.BatchStream(nf, flen, bs)
+        dig = torch.empty((nf * flen // bs, 20), dtype=torch.uint8, device=gpu)
+        assert st.push(data, dig) is None
+        (fh,) = st.finish()
+    else:
+        dig, _, fh = device.index_device_batch(data, [(i * flen, flen) for i in range(nf)], bs)
+    dig, fh = dig.cpu().numpy(), fh.cpu().numpy()
+    host_bytes = data.cpu().numpy()
+    del data
+    torch.cuda.empty_cache()
+    want = oracle.index_fixed_mt(host_bytes, bs, _threads())
+    bad = np.nonzero((dig != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} digests differ, first at block {bad[:5]}"
+    per_file = want.reshape(nf, -1, 20)
+    wrong = [f for f in range(nf) if bytes(fh[f]) != host.blocks_hash(per_file[f])]
+    assert not wrong, f"{len(wrong)} blocks_hash differ, first files {wrong[:5]}"
