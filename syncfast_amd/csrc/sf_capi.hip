@@ -642,14 +642,65 @@ struct FileStage {
   uint64_t rows = 0;
 };
 
+// Page-cache-resident large files of a stage, mapped and page-locked in place
+// so their bytes go to the device by DMA straight from the page cache (no
+// pread copy into the pinned stage).  Released once the stage's copies are
+// done (its event has completed, or the streams are synchronised).
+struct StageMaps {
+  std::vector<std::pair<void*, uint64_t>> m;
+  void release() {
+    for (auto& x : m) {
+      (void)hipHostUnregister(x.first);
+      munmap(x.first, x.second);
+    }
+    m.clear();
+  }
+  ~StageMaps() { release(); }
+};
+
+constexpr uint64_t kMapMinBytes = 4ull << 20;  // smaller files: pread (registration cost per file)
+
+// mapped[k] = the k-th file of the stage is mapped + registered (at ptrs[k]).
+void map_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, StageMaps& maps,
+               std::vector<const uint8_t*>& ptrs) {
+  ptrs.assign(st.files.size(), nullptr);
+  const char* nomm = getenv("SF_NO_MMAP");
+  if (nomm && atoi(nomm)) return;
+  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+  std::vector<unsigned char> res;
+  for (size_t k = 0; k < st.files.size(); k++) {
+    const uint64_t n = size[st.files[k]];
+    if (n < kMapMinBytes) continue;
+    const int fd = open(paths[st.files[k]], O_RDONLY);
+    if (fd < 0) continue;  // the pread route reports the error
+    struct stat sb;
+    void* m = (fstat(fd, &sb) == 0 && (uint64_t)sb.st_size == n) ? mmap(nullptr, n, PROT_READ, MAP_SHARED, fd, 0)
+                                                                  : MAP_FAILED;
+    close(fd);
+    if (m == MAP_FAILED) continue;
+    res.resize(ceil_div(n, pg));
+    uint64_t resident = 0;
+    if (mincore(m, n, res.data()) == 0)
+      for (unsigned char r : res) resident += r & 1u;
+    if (resident * 10 >= res.size() * 9 && hipHostRegister(m, n, hipHostRegisterReadOnly) == hipSuccess) {
+      maps.m.push_back({m, n});
+      ptrs[k] = static_cast<const uint8_t*>(m);
+    } else {
+      (void)hipGetLastError();
+      munmap(m, n);
+    }
+  }
+}
+
 // Fill `dst` with the stage's files: (file, <=16 MiB slice) work items taken
 // by up to 8 threads from an atomic counter.
 int read_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, uint8_t* dst,
-               std::atomic<int64_t>& bad) {
+               std::atomic<int64_t>& bad, const std::vector<const uint8_t*>& mapped) {
   constexpr uint64_t kSlice = 16ull << 20;
   struct Item { uint32_t k; uint64_t a, b; };
   std::vector<Item> items;
   for (uint32_t k = 0; k < st.files.size(); k++) {
+    if (mapped[k]) continue;  // goes to the device straight from its mapping
     const uint64_t n = size[st.files[k]];
     for (uint64_t a = 0; a < n; a += kSlice) items.push_back({k, a, std::min(n, a + kSlice)});
   }
@@ -783,6 +834,8 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     }
   };
   std::atomic<int64_t> bad{-1};
+  StageMaps maps[2];
+  std::vector<const uint8_t*> mptr;
   for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const FileStage& st = stages[k];
@@ -790,13 +843,30 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
       if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
       harvest(k - 2);
     }
-    rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad);
+    maps[b].release();  // stage k-2's copies are done (its event was waited for above)
+    map_stage(paths, st, size, maps[b], mptr);
+    rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad, mptr);
     if (rc) break;
     hipStream_t s = sts.s[b];
-    if (st.bytes && hipMemcpyAsync(ddata[b].p, pin[b].p, st.bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
-      rc = SF_ENODEV;
-      break;
+    // H2D: each mapped file from its mapping, every run of consecutive
+    // pread files from the pinned stage in one copy.
+    uint8_t* dd = static_cast<uint8_t*>(ddata[b].p);
+    const uint8_t* pp = static_cast<const uint8_t*>(pin[b].p);
+    for (size_t j = 0; j < st.files.size() && rc == SF_OK;) {
+      const uint64_t o = st.desc[j].offset;
+      if (mptr[j]) {
+        if (st.desc[j].len && hipMemcpyAsync(dd + o, mptr[j], st.desc[j].len, hipMemcpyHostToDevice, s) != hipSuccess)
+          rc = SF_ENODEV;
+        j++;
+        continue;
+      }
+      size_t e = j;
+      while (e < st.files.size() && !mptr[e]) e++;
+      const uint64_t end = e < st.files.size() ? st.desc[e].offset : st.bytes;
+      if (end > o && hipMemcpyAsync(dd + o, pp + o, end - o, hipMemcpyHostToDevice, s) != hipSuccess) rc = SF_ENODEV;
+      j = e;
     }
+    if (rc) break;
     uint64_t nb = 0;
     rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
                                max_rows, dfh[b].p, nullptr, &nb, s);
@@ -810,6 +880,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
   }
   for (int i = 0; i < 2; i++)
     if (hipStreamSynchronize(sts.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  for (int i = 0; i < 2; i++) maps[i].release();  // every copy has completed
   if (rc == SF_OK)
     for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size(); k++) harvest(k);
   for (int i = 0; i < 2; i++) (void)hipEventDestroy(done[i]);
