@@ -79,18 +79,18 @@ def test_index_files_matches_one_file_path(gpu, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("no_mmap", ["0", "1"])
-@pytest.mark.parametrize("stage", [0, 20 << 20])
+@pytest.mark.parametrize("stage", [0, 160 << 20])
 def test_index_files_large_mapped_and_pread(gpu, tmp_path, stage, no_mmap, monkeypatch):
-    """Files >= 4 MiB that are in the page cache go to the device straight
+    """Files >= 64 MiB that are in the page cache go to the device straight
     from their mappings; smaller ones through the pread stage.  Mixed in one
-    stage (ragged route) and as equal 8 MiB files (staged route); SF_NO_MMAP=1
+    stage (ragged route) and as equal files (staged route); SF_NO_MMAP=1
     forces pread for all.  Same rows either way."""
     monkeypatch.setenv("SF_NO_MMAP", no_mmap)
-    sizes = [5 << 20, 100_000, (4 << 20) + 13, 0, 6 << 20, 77]
+    sizes = [(64 << 20) + 4096, 100_000, (64 << 20) + 13, 0, 5 << 20, 77]
     paths = _write(tmp_path, sizes, 2100)
     rows, first, fh = host.index_files(paths, 4096, stage_bytes=stage)
     _check(paths, sizes, 2100, 4096, rows, first, fh)
-    eq = [8 << 20] * 3
+    eq = [64 << 20] * 2
     paths = _write(tmp_path, eq, 2200)
     rows, first, fh = host.index_files(paths, 4096, stage_bytes=stage)
     _check(paths, eq, 2200, 4096, rows, first, fh)
