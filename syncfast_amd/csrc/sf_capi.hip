@@ -455,9 +455,14 @@ int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t
     cj[k].lo = j.part == 2 ? half : 0;
     cj[k].hi = j.part == 1 ? half : data_ch;
     cj[k].part = j.part;
-    cj[k].wgs = (uint32_t)ceil_div(j.n_files, 64 * sf::kWavesPerWG);
+    cj[k].waves = (uint32_t)ceil_div(j.n_files, 64);  // chain waves, one per workgroup
   }
-  const unsigned grid = cj[0].wgs + cj[1].wgs + (total ? grid_for_blocks(total) : 0u);
+  // grid: C mixed workgroups (1 chain wave + 3 block waves), then 4 block
+  // waves per workgroup for the rest
+  const uint64_t C_ = cj[0].waves + cj[1].waves;
+  const uint64_t bwaves = ceil_div(total, 64);
+  const uint64_t rest = bwaves > 3 * C_ ? bwaves - 3 * C_ : 0;
+  const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
   if (grid == 0) return SF_OK;
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),
                      static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,

@@ -301,12 +301,11 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 // `group` of it (4 waves x 64 consecutive blocks): the body of
 // sha1_fixed_kernel and of the block part of sha1_fixed_chained_kernel.
 template <int TILE, bool WEAK>
-__device__ __forceinline__ void fixed_group(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs,
-                                            uint64_t nblocks, uint8_t* __restrict__ digests, const PadSchedule pad,
-                                            uint32_t* __restrict__ weak, uint32_t group, uint4* __restrict__ smem) {
+__device__ __forceinline__ void fixed_wave(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs,
+                                           uint64_t nblocks, uint8_t* __restrict__ digests, const PadSchedule pad,
+                                           uint32_t* __restrict__ weak, uint64_t wave, uint4* __restrict__ tile) {
   const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
-  const uint64_t first = ((uint64_t)group * kWavesPerWG + wid) * 64;
+  const uint64_t first = wave * 64;  // this wave's 64 consecutive blocks
   if (first >= nblocks) return;
   const uint64_t blk = first + lane;
   const bool valid = blk < nblocks;
@@ -327,7 +326,7 @@ __device__ __forceinline__ void fixed_group(const uint8_t* __restrict__ data, ui
 
   Sha1 st;
   Adler wk;
-  hash_wave<TILE, true, WEAK>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad, wk);
+  hash_wave<TILE, true, WEAK>(data, off, size, rel, valid, geo, tile, st, pad, wk);
   if (valid) {
     st.store(digests + blk * 20);
     if constexpr (WEAK) weak[blk] = wk.fin();
@@ -341,7 +340,9 @@ __global__ void __launch_bounds__(kThreads, WPE)
 sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
                   uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  fixed_group<TILE, WEAK>(data, len, bs, nblocks, digests, pad, weak, blockIdx.x, smem);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
+  fixed_wave<TILE, WEAK>(data, len, bs, nblocks, digests, pad, weak, (uint64_t)blockIdx.x * kWavesPerWG + wid,
+                         smem + wid * 64 * (TILE / 16));
 }
 
 // Stream a 64-B-multiple byte range [lo, hi) of a lane's message through
@@ -474,16 +475,15 @@ struct ChainJob {
   const uint8_t* runs;
   uint8_t* state;
   uint8_t* hashes;
-  uint32_t files, run_len, lo, hi, part, wgs;
+  uint32_t files, run_len, lo, hi, part, waves;  // waves = chain waves (64 files each)
 };
 
 #ifndef SF_CHAIN_DEPTH
 #define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
 #endif
-__device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t g) {
+__device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave) {
   __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t f = (g * kWavesPerWG + wid) * 64 + (threadIdx.x & 63);
+  const uint32_t f = wave * 64 + (threadIdx.x & 63);
   if (f >= j.files) return;
   const uint8_t* p = j.runs + (uint64_t)f * j.run_len;
   uint32_t* sv = reinterpret_cast<uint32_t*>(j.state + (uint64_t)f * 20);
@@ -508,7 +508,7 @@ __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t g) {
 }
 
 // Equal-size many-file batches as a stream (BASELINE configs[2], batch after
-// batch): ONE launch hashes every block of batch i (fixed_group) and, in its
+// batch): ONE launch hashes every block of batch i (fixed_wave) and, in its
 // first workgroups, up to two chain jobs of earlier batches (j0 then j1):
 // with split chains, the second half of batch i-2's and the first half of
 // batch i-1's.  Their digest tables and saved states were completed by
@@ -520,19 +520,27 @@ __global__ void __launch_bounds__(kThreads, 1)
 sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
                           uint8_t* __restrict__ digests, const PadSchedule pad, const ChainJob j0,
                           const ChainJob j1) {
+  // Chain waves are spread one per workgroup: workgroup g < C runs chain
+  // wave g as its wave 0 (job 0's waves first) and block waves 3g..3g+2 as
+  // its waves 1-3; the other workgroups run 4 block waves each.  So no CU
+  // hosts more than one chain wave per workgroup, and the chains' scattered
+  // digest loads are spread over C CUs instead of C/4.
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  uint32_t g = blockIdx.x;
-  if (g < j0.wgs) {
-    chain_job(j0, g);
-    return;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t C = j0.waves + j1.waves;  // chain waves
+  const uint32_t g = blockIdx.x;
+  uint64_t bw;
+  if (g < C) {
+    if (wid == 0) {
+      if (g < j0.waves) chain_job(j0, g);
+      else chain_job(j1, g - j0.waves);
+      return;
+    }
+    bw = (uint64_t)g * 3 + (wid - 1);
+  } else {
+    bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
   }
-  g -= j0.wgs;
-  if (g < j1.wgs) {
-    chain_job(j1, g);
-    return;
-  }
-  g -= j1.wgs;
-  fixed_group<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, g, smem);
+  fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, bw, smem + wid * 64 * (TILE / 16));
 }
 
 #ifdef SF_TUNING
