@@ -341,6 +341,12 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
                   uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
+#if defined(SF_PRIO_EXP) && SF_PRIO_EXP == 1
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);  // A/B only: static priority for half the workgroups
+#elif defined(SF_PRIO_EXP) && SF_PRIO_EXP == 2
+  if (blockIdx.x % 3 == 1) __builtin_amdgcn_s_setprio(1);
+  else if (blockIdx.x % 3 == 2) __builtin_amdgcn_s_setprio(2);
+#endif
   fixed_wave<TILE, WEAK>(data, len, bs, nblocks, digests, pad, weak, (uint64_t)blockIdx.x * kWavesPerWG + wid,
                          smem + wid * 64 * (TILE / 16));
 }
