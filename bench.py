@@ -42,6 +42,18 @@ from syncfast_amd.shard import gather_digests, shard_range  # noqa: E402
 
 GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+# SHA-1 is VALU-issue bound: 613 VALU per 64-B
+# compression, 400 half-rate (4 SIMD-cycles per wave64 op) + 213 full-rate
+# (2 cycles); the uniform padding chunk of a 64-B-multiple block ~1120 cycles.
+SIMDS, MAX_CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMD-32, MI355X_MICROARCH.md
+
+
+def valu_ceiling_gbs(bs):
+    """Input bytes/s the SIMDs can hash at the max clock under the op-cost
+    model above (one lane per block, 64 blocks per wave)."""
+    full, rem = divmod(bs, 64)
+    per_block = full * (400 * 4 + 213 * 2) + (1120 if rem == 0 else (400 * 4 + 213 * 2) * (1 + (rem >= 56)))
+    return SIMDS * MAX_CLOCK_HZ * 64 * bs / per_block / 1e9
 SEED = 0x5EED0000
 
 CONFIGS = {
@@ -323,6 +335,12 @@ def main():
                                 "sha1_fixed_kernel<128%s>" % (", 1, true" if weaks is not None else "")),
                      "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
+        "valu_roofline": None if weaks is not None else {
+            "bound": "valu", "achieved": round(total_bytes / world / (kern_ms * 1e-3) / 1e9, 1),
+            "peak": round(valu_ceiling_gbs(bs), 1), "unit": "GB/s of input",
+            "frac": round(total_bytes / world / (kern_ms * 1e-3) / 1e9 / valu_ceiling_gbs(bs), 4),
+            "model": "613 VALU per 64-B SHA-1 compression (400 at 4 + 213 at 2 SIMD-cycles), 1024 SIMDs at 2.4 GHz; "
+                     "the chip holds ~2.1 GHz under this load (DESIGN.md section 4)"},
         "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
