@@ -266,3 +266,34 @@ def test_max_block_size(gpu):
     assert np.array_equal(d.cpu().numpy(), want)
     with pytest.raises(SfError):
         device.index_device(to_dev(b"x" * 100, gpu), bs + 1)
+
+
+def test_concurrent_host_threads_own_streams(gpu):
+    # include/syncfast_amd.h: device entry points may be called from several
+    # host threads on different streams -- every result still exact
+    import threading
+    bufs = [oracle.splitmix_bytes(4096 * 300 + 17 * k, 600 + k) for k in range(4)]
+    outs, errs = [None] * 4, []
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream(device=gpu)
+            with torch.cuda.stream(s):
+                t = to_dev(bufs[k].tobytes(), gpu)
+                for _ in range(3):
+                    d = device.index_device(t, 4096, stream=s)
+                    w = device.index_device_weak(t, 4096, stream=s)[0]
+                s.synchronize()
+                outs[k] = (d.cpu().numpy(), w.cpu().numpy())
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for k in range(4):
+        want = oracle.index_fixed(bufs[k], 4096)[2]
+        assert np.array_equal(outs[k][0], want) and np.array_equal(outs[k][1], want)
