@@ -26,6 +26,9 @@ extern "C" void sf_host_sha1_impl(const uint8_t* data, uint64_t len, uint8_t out
 namespace {
 
 constexpr int kTile = 128;  // bytes of each block staged per LDS step
+#ifndef SF_FIXED_WPE
+#define SF_FIXED_WPE 1  // min waves/SIMD of the shipped fixed kernel (A/B: make variant EXTRA=-DSF_FIXED_WPE=4)
+#endif
 
 #ifdef SF_TUNING
 inline int variant_choice() {
@@ -110,7 +113,7 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
     default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
   }
 #else
-  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
+  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, SF_FIXED_WPE>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
 #endif
   return hip_err(hipGetLastError());
 }
