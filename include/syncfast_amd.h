@@ -152,6 +152,14 @@ int sf_wire_file_blocks_device(const void *d_digests, uint64_t n_blocks, uint32_
                                uint64_t file_len, void *d_out, uint64_t cap, uint64_t *n_out,
                                void *stream);
 
+/* The same FILE_BLOCK run written to a file descriptor (the SSH pipe of
+ * src/sync/ssh/mod.rs, or a file), streamed: the device builds ~1M messages
+ * at a time, each chunk comes back by DMA into pinned memory and is written
+ * while the device builds the next.  d_digests may still be in production on
+ * `stream` (the copy waits for it).  *n_written = bytes written.  Blocking. */
+int sf_wire_file_blocks_fd(const void *d_digests, uint64_t n_blocks, uint32_t block_size,
+                           uint64_t file_len, int fd, uint64_t *n_written, void *stream);
+
 /* Deterministic synthetic input (bench / tests): bytes [start, start+len)
  * of the splitmix64 stream with this seed. */
 int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t start, void *stream);

@@ -56,6 +56,24 @@ def main():
     finally:
         os.unlink(path)
     many_files(data, d)
+    wire_rate()
+
+
+def wire_rate():
+    """FILE_BLOCK run of config 2's table (2^21 blocks) streamed to a file
+    descriptor (/dev/null: device build + D2H + write syscalls)."""
+    from syncfast_amd import device, wire
+    n = 8 << 30
+    t = device.splitmix_tensor(n, 0x5EED0000)
+    dig = device.index_device(t, 4096)
+    torch.cuda.synchronize()
+    with open("/dev/null", "wb") as f:
+        wire.file_blocks_to_fd(dig, 4096, n, f.fileno())  # warm up
+        t0 = time.perf_counter()
+        nbytes = wire.file_blocks_to_fd(dig, 4096, n, f.fileno())
+        dt = time.perf_counter() - t0
+    print(f"wire: FILE_BLOCK run of 2^21 blocks ({nbytes / 1e6:.1f} MB) to an fd: {nbytes / dt / 1e9:.2f} GB/s "
+          f"({dig.shape[0] / dt / 1e6:.1f} M messages/s)", flush=True)
 
 
 def many_files(data, d):

@@ -5,6 +5,7 @@
 // implementation of the block hashing in this library: without a HIP device
 // the device entry points return SF_ENODEV.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <stdint.h>
 #include <sys/mman.h>
@@ -491,6 +492,79 @@ int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_
   hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, as_stream(stream),
                      static_cast<const uint8_t*>(d_digests), nb, block_size, last, static_cast<uint8_t*>(d_out));
   return hip_err(hipGetLastError());
+}
+
+int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
+                           uint64_t* n_written, void* stream) {
+  if (n_written) *n_written = 0;
+  if (block_size == 0 || block_size > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
+  const uint64_t nb = file_len ? ceil_div(file_len, block_size) : 0;
+  if (nb != n_blocks) return SF_EINVAL;
+  if (!nb) return SF_OK;
+  if (!d_digests || fd < 0) return SF_EINVAL;
+  uint64_t db = 1;
+  for (uint64_t v = block_size; v >= 10; v /= 10) db++;
+  const uint32_t last = (uint32_t)(file_len - (nb - 1) * block_size);
+  uint64_t dl = 1;
+  for (uint64_t v = last; v >= 10; v /= 10) dl++;
+  const uint64_t msg = 33 + db;  // every message but the last
+  const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
+  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : (1ull << 20));
+  const uint64_t nchunks = ceil_div(nb, per);
+  const uint64_t cap = std::min(per, nb) * msg + (33 + dl);
+  Streams st;
+  DevBuf dout[2];
+  PinBuf pin[2];
+  hipEvent_t ev[2] = {nullptr, nullptr}, ready = nullptr;
+  uint64_t bytes_of[2] = {0, 0};
+  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  SF_HIP(hipEventRecord(ready, as_stream(stream)));  // the digests are produced on the caller's stream
+  for (int i = 0; i < 2; i++) {
+    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
+    SF_HIP(hipStreamWaitEvent(st.s[i], ready, 0));
+    SF_HIP(hipMalloc(&dout[i].p, cap));
+    SF_HIP(hipHostMalloc(&pin[i].p, cap, hipHostMallocDefault));
+    SF_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  }
+  uint64_t written = 0;
+  int rc = SF_OK;
+  auto flush = [&](int b) {  // write chunk buffer b to fd, in order
+    if (hipEventSynchronize(ev[b]) != hipSuccess) return SF_ENODEV;
+    const uint8_t* p = static_cast<const uint8_t*>(pin[b].p);
+    for (uint64_t done = 0; done < bytes_of[b];) {
+      const ssize_t w = write(fd, p + done, bytes_of[b] - done);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return SF_EIO;
+      done += (uint64_t)w;
+      written += (uint64_t)w;
+    }
+    return SF_OK;
+  };
+  // chunk k: device builds its messages, D2H into pin[k&1]; the host writes
+  // chunk k-2 while the device works on chunk k.
+  for (uint64_t k = 0; k < nchunks && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (k >= 2 && (rc = flush(b)) != SF_OK) break;
+    const uint64_t i0 = k * per, n = std::min(per, nb - i0);
+    const bool final_chunk = i0 + n == nb;
+    const uint32_t lsz = final_chunk ? last : block_size;
+    bytes_of[b] = (n - 1) * msg + (final_chunk ? 33 + dl : msg);
+    hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st.s[b],
+                       static_cast<const uint8_t*>(d_digests) + i0 * 20, n, block_size, lsz,
+                       static_cast<uint8_t*>(dout[b].p));
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(pin[b].p, dout[b].p, bytes_of[b], hipMemcpyDeviceToHost, st.s[b]) != hipSuccess ||
+        hipEventRecord(ev[b], st.s[b]) != hipSuccess)
+      rc = SF_ENODEV;
+  }
+  for (uint64_t k = nchunks >= 2 ? nchunks - 2 : 0; k < nchunks && rc == SF_OK; k++) rc = flush((int)(k & 1));
+  for (int i = 0; i < 2; i++) {
+    (void)hipStreamSynchronize(st.s[i]);
+    (void)hipEventDestroy(ev[i]);
+  }
+  (void)hipEventDestroy(ready);
+  if (n_written) *n_written = written;
+  return rc;
 }
 
 int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t start, void* stream) {

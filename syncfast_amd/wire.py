@@ -61,3 +61,18 @@ def file_blocks_device(digests, block_size: int, file_len: int, stream=None):
         check(lib().sf_wire_file_blocks_device(digests.data_ptr(), n, block_size, file_len, out.data_ptr(),
                                                out.numel(), ctypes.byref(need), s), "sf_wire_file_blocks_device")
     return out
+
+
+def file_blocks_to_fd(digests, block_size: int, file_len: int, fd: int, stream=None) -> int:
+    """The FILE_BLOCK run of a fixed-tiled file written to a file descriptor
+    (an SSH pipe or a file): built on the device in chunks, streamed back by
+    DMA and written while the next chunk is built (sf_wire_file_blocks_fd).
+    Returns the bytes written."""
+    import torch
+    n = digests.shape[0]
+    s = (stream or torch.cuda.current_stream(digests.device)).cuda_stream
+    out = ctypes.c_uint64(0)
+    with torch.cuda.device(digests.device):
+        check(lib().sf_wire_file_blocks_fd(digests.data_ptr() if n else None, n, block_size, file_len, fd,
+                                           ctypes.byref(out), s), "sf_wire_file_blocks_fd")
+    return out.value

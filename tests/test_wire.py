@@ -33,3 +33,24 @@ def test_file_blocks_device_matches_write_message(gpu, n, bs):
     _, sizes, want_d = oracle.index_fixed(data, bs)
     want = b"".join(wire.write_message("FileBlock", bytes(dd), int(sz)) for dd, sz in zip(want_d, sizes))
     assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", ["1", "7", "1000", "0"])
+@pytest.mark.parametrize("n,bs", [(4096 * 2500 + 7, 4096), (999, 100), (4096, 4096)])
+def test_file_blocks_to_fd_streams_the_same_bytes(gpu, tmp_path, monkeypatch, n, bs, chunk):
+    # the streamed writer (chunks of SF_WIRE_CHUNK messages, double-buffered
+    # D2H, in-order writes) produces exactly the device-built run
+    if chunk != "0":
+        monkeypatch.setenv("SF_WIRE_CHUNK", chunk)
+    data = oracle.splitmix_bytes(n, n + 1)
+    t = torch.from_numpy(data.copy()).to(gpu)
+    dig = device.index_device(t, bs)
+    want = wire.file_blocks_device(dig, bs, n).cpu().numpy().tobytes()
+    p = tmp_path / "wire.bin"
+    with open(p, "wb") as f:
+        got_n = wire.file_blocks_to_fd(dig, bs, n, f.fileno())
+    assert got_n == len(want) and p.read_bytes() == want
+    if n < 10_000:
+        _, sizes, want_d = oracle.index_fixed(data, bs)
+        assert want == b"".join(wire.write_message("FileBlock", bytes(dd), int(sz)) for dd, sz in zip(want_d, sizes))
