@@ -14,6 +14,8 @@
  * cut.  Research tool: nothing in the product or the tests links it.
  *
  *   gcc -O2 -o /tmp/cdc_search scripts/cdc_search.c && /tmp/cdc_search
+ *   gcc -O2 -DMINSIZE -o /tmp/cdc_min scripts/cdc_search.c && /tmp/cdc_min
+ *     (min-size gate: is 11579 a trigger at all, and which min sizes M fit)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -113,6 +115,7 @@ static int run(const Hyp* y, int* first) {
   return ncut == 2;
 }
 
+#ifndef MINSIZE
 int main(void) {
   n = 0;
   for (int i = 1; i <= 2000; ++i) n += sprintf((char*)buf + n, "Line %d\n", i);
@@ -148,3 +151,36 @@ int main(void) {
          "zpaq form (h+c+1)*M, h<2^19 -> first cut %d\n", tried, first_ok, full, f);
   return 0;
 }
+#else
+/* (a) predicate gated by chunk size >= M (hash runs from chunk start, reset at cuts). */
+static int trig[64<<10];
+static int scan(const Hyp* y, int start, int end, int resetwhat, St* s0) {
+  St s; if (s0) s=*s0; else memset(&s,0,sizeof s);
+  int nt=0;
+  for (int i=start;i<end;i++){ upd(&s,y,buf[i]); if(pred(y,s.h)) trig[nt++]=i+1-start; }
+  return nt;
+}
+int main(void) {
+  n=0; for(int i=1;i<=2000;++i) n+=sprintf((char*)buf+n,"Line %d\n",i);
+  for(int i=0;i<2000;++i) n+=sprintf((char*)buf+n,"Test content\n");
+  Hyp y; long tried=0, hits=0;
+  for (y.w64 = 0; y.w64 < 2; ++y.w64)
+  for (y.mp = 0; y.mp < NPAIRS; ++y.mp)
+  for (y.form = 0; y.form < 7; ++y.form)
+  for (y.ctx = 0; y.ctx < 4; ++y.ctx)
+  for (y.pred = 0; y.pred < 6; ++y.pred)
+  for (y.k = 1; y.k <= (y.w64 ? 63 : 31); ++y.k) {
+    ++tried;
+    int nt = scan(&y, 0, 11579, 0, 0);
+    if (nt==0 || trig[nt-1]!=11579) continue;
+    int lo = nt>1 ? trig[nt-2]+1 : 1;   /* M must exceed the previous trigger */
+    /* second chunk, fresh state: no trigger with size >= M within 32768 */
+    int nt2 = scan(&y, 11579, 44347, 0, 0);
+    int mx2 = 0; for (int j=0;j<nt2;j++) if (trig[j] < 32768) mx2 = trig[j];
+    /* need every trigger in chunk 2 (< 32768) to be < M  => M > mx2 */
+    int M_lo = lo > mx2+1 ? lo : mx2+1;
+    if (M_lo <= 11579) { ++hits; printf("w64=%d mp=%d form=%d ctx=%d pred=%d k=%d  M in [%d, 11579] (prev trig %d, chunk2 max trig %d, ntrig %d)\n", y.w64,y.mp,y.form,y.ctx,y.pred,y.k, M_lo, nt>1?trig[nt-2]:-1, mx2, nt); }
+  }
+  printf("tried %ld, %ld consistent with a min size\n", tried, hits);
+}
+#endif
