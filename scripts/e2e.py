@@ -34,25 +34,35 @@ def main():
     torch.cuda.synchronize()
     print("pinned H2D (torch, 4x1 GiB):", rate(4 << 30, time.perf_counter() - t0), flush=True)
     host.index_buffer(data[: 256 << 20], 4096)  # warm up
-    for knob in ("0", "1"):
-        os.environ["SF_NO_HOSTREG"] = knob
-        t0 = time.perf_counter()
-        rows = host.index_buffer(data, 4096)
-        t = time.perf_counter() - t0
-        print(f"sf_index_buffer {n / GiB:.0f} GiB, 4 KiB blocks, {'staged memcpy' if knob == '1' else 'hostRegister'}:",
-              rate(n, t), flush=True)
+    # in place (regions locked one ahead, rows + blocks_hash overlapped), in
+    # place serial (whole range locked first, rows after: the earlier form),
+    # staged through pinned buffers
+    routes = (("in place, overlapped", {}), ("in place, serial", {"SF_INPLACE_SERIAL": "1"}),
+              ("staged memcpy", {"SF_NO_HOSTREG": "1"}))
+    for rep in range(2):
+        for name, env in routes:
+            os.environ.update(env)
+            t0 = time.perf_counter()
+            rows = host.index_buffer(data, 4096)
+            t = time.perf_counter() - t0
+            for k in env:
+                del os.environ[k]
+            print(f"sf_index_buffer {n / GiB:.0f} GiB, 4 KiB blocks, {name} (rep {rep}):", rate(n, t), flush=True)
     assert rows.shape[0] == n // 4096
     d = os.environ.get("E2E_DIR", "/tmp")
     with tempfile.NamedTemporaryFile(dir=d, delete=False) as f:
         f.write(data.tobytes())
         path = f.name
     try:
-        for i in range(2):
+        for i, env in enumerate([{}, {}, {"SF_INPLACE_SERIAL": "1"}, {}, {"SF_INPLACE_SERIAL": "1"}]):
+            os.environ.update(env)
             t0 = time.perf_counter()
             rows, bh = host.index_file(path, 4096)
             t = time.perf_counter() - t0
-            print(f"sf_index_file {n / GiB:.0f} GiB ({'cold-ish' if i == 0 else 'page cache'}), incl. blocks_hash:",
-                  rate(n, t), flush=True)
+            for k in env:
+                del os.environ[k]
+            what = "cold-ish" if i == 0 else "page cache, " + ("serial" if env else "overlapped")
+            print(f"sf_index_file {n / GiB:.0f} GiB ({what}), incl. blocks_hash:", rate(n, t), flush=True)
     finally:
         os.unlink(path)
     many_files(data, d)

@@ -13,6 +13,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+
+#include "host_sha1.h"
+
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -133,3 +137,50 @@ extern "C" void sf_host_sha1_impl(const uint8_t* data, uint64_t len, uint8_t out
 }
 
 extern "C" int sf_host_has_shani(void) { return sfh::have_shani() ? 1 : 0; }
+
+// Streaming form (internal to the library, not in include/): the in-place
+// host pipelines fold each stage's digests into a file's blocks_hash while the
+// next stage is still on the PCIe link (src/index.rs:661-682 hashes the
+// concatenated digests in order).
+extern "C" void sf_host_sha1_begin(sf_host_sha1_stream* s) {
+  static const uint32_t iv[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  memcpy(s->h, iv, sizeof iv);
+  s->nbuf = 0;
+  s->total = 0;
+  s->shani = sfh::have_shani() ? 1 : 0;
+}
+
+extern "C" void sf_host_sha1_update(sf_host_sha1_stream* s, const uint8_t* p, uint64_t n) {
+  s->total += n;
+  if (s->nbuf) {
+    const uint64_t take = std::min<uint64_t>(64 - s->nbuf, n);
+    memcpy(s->buf + s->nbuf, p, take);
+    s->nbuf += (uint32_t)take;
+    p += take;
+    n -= take;
+    if (s->nbuf < 64) return;
+    sfh::compress(s->h, s->buf, 1, s->shani);
+    s->nbuf = 0;
+  }
+  const uint64_t full = n / 64;
+  if (full) sfh::compress(s->h, p, full, s->shani);
+  s->nbuf = (uint32_t)(n - full * 64);
+  if (s->nbuf) memcpy(s->buf, p + full * 64, s->nbuf);
+}
+
+extern "C" void sf_host_sha1_final(sf_host_sha1_stream* s, uint8_t out[20]) {
+  uint8_t tail[128];
+  memset(tail, 0, sizeof tail);
+  if (s->nbuf) memcpy(tail, s->buf, s->nbuf);
+  tail[s->nbuf] = 0x80;
+  const size_t tblocks = s->nbuf < 56 ? 1 : 2;
+  const uint64_t bits = s->total * 8u;
+  for (int i = 0; i < 8; i++) tail[tblocks * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+  sfh::compress(s->h, tail, tblocks, s->shani);
+  for (int i = 0; i < 5; i++) {
+    out[4 * i] = (uint8_t)(s->h[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(s->h[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(s->h[i] >> 8);
+    out[4 * i + 3] = (uint8_t)s->h[i];
+  }
+}

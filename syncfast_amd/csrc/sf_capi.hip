@@ -22,7 +22,11 @@
 #include "../../include/syncfast_amd.h"
 #include "sf_kernels.hpp"
 
-extern "C" void sf_host_sha1_impl(const uint8_t* data, uint64_t len, uint8_t out[20], int force_scalar);
+#include "host_sha1.h"
+
+// Internal status of the in-place route (never returned through the C-ABI):
+// the caller's pages could not be page-locked, take the staged route.
+#define SF_ENOTSUP (-95)
 
 namespace {
 
@@ -577,15 +581,67 @@ int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t s
   return hip_err(hipGetLastError());
 }
 
-// Host buffer that is (or was made) page-locked: the DMA engine reads it in
-// place, stage by stage, overlapped with the kernel of the previous stage.
-static int index_registered(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
-                     uint64_t* n_out) {
+// In-place route of sf_index_buffer / sf_index_file: the DMA engine reads the
+// caller's pages (or the page-cache pages of a mapped file) directly, no
+// staging memcpy.  Per ~256 MiB stage, on alternating streams: H2D, the
+// block kernel, D2H of the stage's digests.  The host overlaps the rest with
+// the PCIe link:
+//   - the pages are page-locked (hipHostRegister) one region ahead of the
+//     copy that reads them, instead of all before the first copy;
+//   - stage k-1's rows are written and its digests folded into the file's
+//     blocks_hash (src/index.rs:661-682) while stage k is on the link.
+// Region k = [page_up(data + k*stage), page_up(data + (k+1)*stage)), so a
+// stage's bytes lie in regions k-1 (its head, up to the first page edge) and
+// k, and no page is registered twice.  A
+// region that cannot be registered after the first one switches the rest of
+// the stages to a pinned bounce buffer (memcpy, one stage at a time): slower,
+// same result.  Returns SF_ENOTSUP (nothing done) when the first
+// region cannot be registered, so the caller can take its staged route.
+// SF_INPLACE_SERIAL=1 registers the whole range first and writes rows and
+// blocks_hash after the last stage (the previous form; A/B knob).
+static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
+                         uint64_t* n_out, uint8_t* blocks_hash) {
   const uint64_t nblocks = ceil_div(len, bs);
   if (n_out) *n_out = nblocks;
   if (nblocks > cap) return SF_ENOSPC;
+  const char* ser = getenv("SF_INPLACE_SERIAL");
+  const bool serial = ser && atoi(ser);
   const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
   const uint64_t nstages = ceil_div(len, stage);
+  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t lo = (uintptr_t)data & ~(uintptr_t)(pg - 1);
+  const uintptr_t hi = ((uintptr_t)data + len + pg - 1) & ~(uintptr_t)(pg - 1);
+  auto edge = [&](uint64_t k) -> uintptr_t {  // start of region k (k = nstages: end of the range)
+    if (k == 0) return lo;
+    if (k >= nstages) return hi;
+    return std::min<uintptr_t>(hi, ((uintptr_t)data + k * stage + pg - 1) & ~(uintptr_t)(pg - 1));
+  };
+  enum { kEmpty, kLocked, kPageable };
+  std::vector<std::pair<void*, int>> regs;  // (region start, state)
+  struct Unreg {
+    std::vector<std::pair<void*, int>>* r;
+    ~Unreg() {
+      for (auto& x : *r)
+        if (x.second == kLocked) (void)hipHostUnregister(x.first);
+    }
+  } unreg{&regs};
+  const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to register
+  const long fail_k = fail_at ? atol(fail_at) : -1;
+  auto reg = [&](uint64_t k) {
+    const uintptr_t a = serial ? lo : edge(k), e = serial ? hi : edge(k + 1);
+    // after one failure every later region stays pageable (a stage straddles
+    // the page it shares with the previous region)
+    if (e <= a) { regs.push_back({(void*)a, kEmpty}); return; }
+    if ((!regs.empty() && regs.back().second == kPageable) || (long)k == fail_k) {
+      regs.push_back({(void*)a, kPageable});
+      return;
+    }
+    const bool ok = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    regs.push_back({(void*)a, ok ? kLocked : kPageable});
+  };
+  reg(0);
+  if (regs[0].second != kLocked) return SF_ENOTSUP;
   Streams st;
   DevBuf ddata[2], ddig;
   PinBuf pdig;
@@ -595,29 +651,78 @@ static int index_registered(const uint8_t* data, uint64_t len, uint32_t bs, sf_b
   }
   SF_HIP(hipMalloc(&ddig.p, nblocks * 20));
   SF_HIP(hipHostMalloc(&pdig.p, nblocks * 20, hipHostMallocDefault));
+  hipEvent_t done[2] = {nullptr, nullptr};
+  struct Evs {
+    hipEvent_t* e;
+    ~Evs() {
+      for (int i = 0; i < 2; i++)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } evs{done};
+  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
+  auto rows = [&](uint64_t k) {  // rows + blocks_hash of stage k (its digests are on the host)
+    const uint64_t b0 = k * stage / bs, b1 = std::min(nblocks, ceil_div((k + 1) * stage, bs));
+    for (uint64_t i = b0; i < b1; i++) {
+      out[i].offset = i * bs;
+      out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
+      memcpy(out[i].sha1, dg + 20 * i, 20);
+    }
+    if (blocks_hash) sf_host_sha1_update(&bh, dg + 20 * b0, (b1 - b0) * 20);
+  };
+  PinBuf bounce;  // only if a region after the first cannot be registered
   int rc = SF_OK;
   for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const uint64_t off = k * stage;
     const uint64_t n = std::min(stage, len - off);
+    const uint64_t b0 = off / bs, nb = ceil_div(n, bs);
+    uint8_t* dd = static_cast<uint8_t*>(ddig.p) + b0 * 20;
+    const uint8_t* src = data + off;
+    if (!serial && regs.back().second == kPageable) {  // region k is not page-locked: bounce
+      for (int i = 0; i < 2; i++)
+        if (hipStreamSynchronize(st.s[i]) != hipSuccess) rc = SF_ENODEV;
+      if (rc != SF_OK) break;
+      if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
+      memcpy(bounce.p, src, n);
+      src = static_cast<const uint8_t*>(bounce.p);
+    }
+    // A copy must lie inside ONE registration: a stage that starts mid-page
+    // copies its head (up to the page edge, in region k-1) separately from
+    // the rest (region k).
+    const uint64_t head = (serial || src != data + off || k == 0) ? 0 : std::min<uint64_t>(n, edge(k) - (uintptr_t)src);
     // stream b is in order: the copy into ddata[b] waits for the kernel of
     // stage k-2 that read it.
-    if (hipMemcpyAsync(ddata[b].p, data + off, n, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) {
+    if ((head && hipMemcpyAsync(ddata[b].p, src, head, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) ||
+        (n > head && hipMemcpyAsync(static_cast<uint8_t*>(ddata[b].p) + head, src + head, n - head,
+                                    hipMemcpyHostToDevice, st.s[b]) != hipSuccess)) {
       rc = SF_ENODEV;
       break;
     }
-    rc = launch_fixed(ddata[b].p, n, bs, ceil_div(n, bs), static_cast<uint8_t*>(ddig.p) + (off / bs) * 20, st.s[b]);
+    rc = launch_fixed(ddata[b].p, n, bs, nb, dd, st.s[b]);
+    if (rc != SF_OK) break;
+    if (!serial) {
+      if (hipMemcpyAsync(static_cast<uint8_t*>(pdig.p) + b0 * 20, dd, nb * 20, hipMemcpyDeviceToHost, st.s[b]) != hipSuccess ||
+          hipEventRecord(done[b], st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+      if (k + 1 < nstages) reg(k + 1);
+      if (k >= 1) {
+        if (hipEventSynchronize(done[b ^ 1]) != hipSuccess) { rc = SF_ENODEV; break; }
+        rows(k - 1);
+      }
+    }
   }
   for (int i = 0; i < 2; i++)
     if (hipStreamSynchronize(st.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   if (rc != SF_OK) return rc;
-  SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
-  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
-  for (uint64_t i = 0; i < nblocks; i++) {
-    out[i].offset = i * bs;
-    out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
-    memcpy(out[i].sha1, dg + 20 * i, 20);
+  if (serial) {
+    SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < nstages; k++) rows(k);
+  } else {
+    rows(nstages - 1);
   }
+  if (blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
   return SF_OK;
 }
 
@@ -630,12 +735,8 @@ int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_b
   // forces the staged path (A/B knob).
   const char* noreg = getenv("SF_NO_HOSTREG");
   if (len >= (64ull << 20) && !(noreg && atoi(noreg))) {
-    if (hipHostRegister(const_cast<uint8_t*>(data), len, hipHostRegisterReadOnly) == hipSuccess) {
-      rc = index_registered(data, len, block_size, out, cap, n_out);
-      (void)hipHostUnregister(const_cast<uint8_t*>(data));
-      return rc;
-    }
-    (void)hipGetLastError();
+    rc = index_inplace(data, len, block_size, out, cap, n_out, nullptr);
+    if (rc != SF_ENOTSUP) return rc;
   }
   return index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
     memcpy(dst, data + off, n);
@@ -671,16 +772,14 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
       uint64_t resident = 0;
       if (mincore(m, len, res.data()) == 0)
         for (unsigned char r : res) resident += r & 1u;
-      if (resident * 10 >= res.size() * 9 &&
-          hipHostRegister(m, len, hipHostRegisterReadOnly) == hipSuccess) {
-        rc = index_registered(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out);
-        (void)hipHostUnregister(m);
-        munmap(m, len);
-        close(fd);
-        if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
-        return rc;
+      if (resident * 10 >= res.size() * 9) {
+        rc = index_inplace(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out, blocks_hash);
+        if (rc != SF_ENOTSUP) {
+          munmap(m, len);
+          close(fd);
+          return rc;
+        }
       }
-      (void)hipGetLastError();
       munmap(m, len);
     }
   }

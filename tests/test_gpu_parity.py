@@ -205,6 +205,46 @@ def test_index_file_large_both_routes(gpu, no_mmap, monkeypatch):
     assert bh == oracle.blocks_hash(want)
 
 
+@pytest.fixture(scope="module")
+def inplace_case():
+    # 2.4 pipeline stages (256 MiB each) + a ragged tail, so stage and
+    # page-lock region edges both fall inside blocks
+    n = 5 * (256 << 20) // 2 + 4093
+    data = oracle.splitmix_bytes(n + 3, 96)
+    return data, oracle.index_fixed_mt(data[3:], 4096, 8)
+
+
+@pytest.mark.parametrize("knob", [("", ""), ("SF_INPLACE_SERIAL", "1"), ("SF_INPLACE_FAIL_AT", "0"),
+                                  ("SF_INPLACE_FAIL_AT", "1"), ("SF_INPLACE_FAIL_AT", "2")])
+def test_index_buffer_inplace_routes(gpu, inplace_case, knob, monkeypatch):
+    # sf_index_buffer page-locks the caller's pages one region ahead of the
+    # copy that reads them; data[3:] is not page-aligned, so a stage reads the
+    # last page of the previous region.  FAIL_AT=0: nothing can be locked
+    # (staged route); FAIL_AT=k>0: regions >= k are copied through a bounce
+    # buffer; SERIAL: whole range locked up front, rows after the last stage.
+    if knob[0]:
+        monkeypatch.setenv(*knob)
+    data, want = inplace_case
+    n = data.size - 3
+    rows = host.index_buffer(data[3:], 4096)
+    assert np.array_equal(rows["sha1"], want)
+    assert rows["offset"][-1] == (n - 1) // 4096 * 4096 and int(rows["size"].sum()) == n
+
+
+@pytest.mark.parametrize("fail_at", ["", "1"])
+def test_index_file_inplace_multi_stage(gpu, inplace_case, fail_at, monkeypatch, tmp_path):
+    # a page-cache-resident file of 2.4 stages: mapped, locked region by
+    # region, blocks_hash folded in stage by stage
+    if fail_at:
+        monkeypatch.setenv("SF_INPLACE_FAIL_AT", fail_at)
+    data, want = inplace_case
+    path = tmp_path / "f.bin"
+    path.write_bytes(data[3:].tobytes())
+    rows, bh = host.index_file(str(path), 4096)
+    assert np.array_equal(rows["sha1"], want)
+    assert bh == oracle.blocks_hash(want)
+
+
 def test_block_digest_independent_of_neighbours(gpu):
     # the same block bytes at different positions / in different waves give
     # the same digest (no cross-lane leakage through the LDS tile)
