@@ -616,7 +616,7 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
     if (k >= nstages) return hi;
     return std::min<uintptr_t>(hi, ((uintptr_t)data + k * stage + pg - 1) & ~(uintptr_t)(pg - 1));
   };
-  enum { kEmpty, kLocked, kPageable };
+  enum { kEmpty, kLocked, kPageable, kPinned };  // kPinned: the caller's pages are already page-locked
   std::vector<std::pair<void*, int>> regs;  // (region start, state)
   struct Unreg {
     std::vector<std::pair<void*, int>>* r;
@@ -625,6 +625,17 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
         if (x.second == kLocked) (void)hipHostUnregister(x.first);
     }
   } unreg{&regs};
+  // A buffer that is already page-locked (hipHostMalloc, or registered by the
+  // caller) is copied from as it is: hipHostRegister would refuse it.
+  auto pinned_at = [](const void* p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return at.type == hipMemoryTypeHost;
+  };
+  const bool prepinned = pinned_at(data) && pinned_at(data + len - 1);
   const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to register
   const long fail_k = fail_at ? atol(fail_at) : -1;
   auto reg = [&](uint64_t k) {
@@ -632,16 +643,19 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
     // after one failure every later region stays pageable (a stage straddles
     // the page it shares with the previous region)
     if (e <= a) { regs.push_back({(void*)a, kEmpty}); return; }
+    if (prepinned) { regs.push_back({(void*)a, kPinned}); return; }
     if ((!regs.empty() && regs.back().second == kPageable) || (long)k == fail_k) {
       regs.push_back({(void*)a, kPageable});
       return;
     }
-    const bool ok = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly) == hipSuccess;
-    if (!ok) (void)hipGetLastError();
-    regs.push_back({(void*)a, ok ? kLocked : kPageable});
+    const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
+    if (err != hipSuccess) (void)hipGetLastError();
+    regs.push_back({(void*)a, err == hipSuccess                               ? kLocked
+                              : err == hipErrorHostMemoryAlreadyRegistered ? kPinned
+                                                                           : kPageable});
   };
   reg(0);
-  if (regs[0].second != kLocked) return SF_ENOTSUP;
+  if (regs[0].second != kLocked && regs[0].second != kPinned) return SF_ENOTSUP;
   Streams st;
   DevBuf ddata[2], ddig;
   PinBuf pdig;

@@ -231,6 +231,17 @@ def test_index_buffer_inplace_routes(gpu, inplace_case, knob, monkeypatch):
     assert rows["offset"][-1] == (n - 1) // 4096 * 4096 and int(rows["size"].sum()) == n
 
 
+def test_index_buffer_already_pinned(gpu, inplace_case):
+    # a caller buffer that is already page-locked (torch pinned memory =
+    # hipHostMalloc): hipHostRegister reports it registered, and the stages
+    # are copied from it in place
+    data, want = inplace_case
+    pinned = torch.empty(data.size, dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = data
+    rows = host.index_buffer(pinned.numpy()[3:], 4096)
+    assert np.array_equal(rows["sha1"], want)
+
+
 @pytest.mark.parametrize("fail_at", ["", "1"])
 def test_index_file_inplace_multi_stage(gpu, inplace_case, fail_at, monkeypatch, tmp_path):
     # a page-cache-resident file of 2.4 stages: mapped, locked region by
