@@ -70,6 +70,11 @@ const char *sf_strerror(int code);
 /* Number of visible HIP devices (0 on a machine without one). */
 int sf_device_count(int *n);
 int sf_set_device(int device);
+/* The host-memory entry points (sf_index_buffer, sf_index_file) keep their
+ * per-device streams, stage buffers and digest tables between calls (setting
+ * them up costs ~8 ms per call).  This frees them; the next call sets them up
+ * again.  Blocks while another thread is inside such a call. */
+int sf_release_host_cache(void);
 
 /* --------------------------------------- device-resident hot path ---- */
 

@@ -27,7 +27,7 @@ MAX_BLOCK_SIZE = 32 << 20
 
 # Every symbol include/syncfast_amd.h declares (checked by the CPU tests).
 EXPORTED = (
-    "sf_version", "sf_strerror", "sf_device_count", "sf_set_device",
+    "sf_version", "sf_strerror", "sf_device_count", "sf_set_device", "sf_release_host_cache",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_file", "sf_index_files",
@@ -72,6 +72,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_strerror.argtypes = [i32]
     L.sf_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     L.sf_set_device.argtypes = [i32]
+    L.sf_release_host_cache.argtypes = []
     L.sf_index_device_fixed.argtypes = [vp, u64, u32, vp, u64, pu64, vp]
     L.sf_index_device_blocks.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp]
     L.sf_index_device_fixed_weak.argtypes = [vp, u64, u32, vp, vp, u64, pu64, vp]

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -206,6 +207,110 @@ struct Streams {
   }
 };
 
+// Per-device resources of the host-memory entry points (streams, events,
+// device stage buffers, digest table, pinned stages), kept between calls:
+// setting them up cost ~8 ms per call (hipMalloc / hipHostMalloc of the
+// stages), ten times the PCIe time of a 64 MiB file.  One call at a time uses
+// a device's set; a concurrent call gets a private set.  Capacities only
+// grow, up to kCacheMax per buffer; a larger buffer is allocated for the call
+// alone.  sf_release_host_cache() frees the sets.  They are never freed from
+// a static destructor: the HIP runtime may already be gone at exit.
+constexpr uint64_t kCacheMax = 512ull << 20;
+constexpr int kMaxDevices = 64;
+
+struct HostRes {
+  hipStream_t s[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  void* dev[3] = {nullptr, nullptr, nullptr};  // stage 0, stage 1, digest table
+  uint64_t dev_cap[3] = {0, 0, 0};
+  void* pin[3] = {nullptr, nullptr, nullptr};  // stage 0, stage 1, digest table
+  uint64_t pin_cap[3] = {0, 0, 0};
+  void free_all() {
+    for (int i = 0; i < 3; i++) {
+      if (dev[i]) (void)hipFree(dev[i]);
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      dev[i] = pin[i] = nullptr;
+      dev_cap[i] = pin_cap[i] = 0;
+    }
+    for (int i = 0; i < 2; i++) {
+      if (s[i]) (void)hipStreamDestroy(s[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      s[i] = nullptr;
+      ev[i] = nullptr;
+    }
+  }
+};
+
+std::mutex g_res_mu[kMaxDevices];
+HostRes* g_res[kMaxDevices];
+
+class HostLease {
+ public:
+  HostLease() {
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices) {
+      lk_ = std::unique_lock<std::mutex>(g_res_mu[d], std::try_to_lock);
+      if (lk_.owns_lock()) {
+        if (!g_res[d]) g_res[d] = new HostRes;
+        r_ = g_res[d];
+        return;
+      }
+    } else {
+      (void)hipGetLastError();
+    }
+    own_ = new HostRes;
+    r_ = own_;
+  }
+  ~HostLease() {
+    for (int i = 0; i < 2; i++)  // an early error return may leave copies in flight
+      if (r_->s[i]) (void)hipStreamSynchronize(r_->s[i]);
+    for (void* p : tmp_dev_) (void)hipFree(p);
+    for (void* p : tmp_pin_) (void)hipHostFree(p);
+    if (own_) {
+      own_->free_all();
+      delete own_;
+    }
+  }
+  HostLease(const HostLease&) = delete;
+  HostLease& operator=(const HostLease&) = delete;
+  int streams(hipStream_t*& s, hipEvent_t*& ev) {
+    for (int i = 0; i < 2; i++) {
+      if (!r_->s[i]) SF_HIP(hipStreamCreateWithFlags(&r_->s[i], hipStreamNonBlocking));
+      if (!r_->ev[i]) SF_HIP(hipEventCreateWithFlags(&r_->ev[i], hipEventDisableTiming));
+    }
+    s = r_->s;
+    ev = r_->ev;
+    return SF_OK;
+  }
+  int dev(int i, uint64_t need, void** out) { return get(r_->dev[i], r_->dev_cap[i], need, false, out); }
+  int pin(int i, uint64_t need, void** out) { return get(r_->pin[i], r_->pin_cap[i], need, true, out); }
+
+ private:
+  int get(void*& slot, uint64_t& cap, uint64_t need, bool pinned, void** out) {
+    need = std::max<uint64_t>(need, 1);
+    if (need <= cap) {
+      *out = slot;
+      return SF_OK;
+    }
+    void* p = nullptr;
+    if (pinned) SF_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
+    else SF_HIP(hipMalloc(&p, need));
+    if (need > kCacheMax) {
+      (pinned ? tmp_pin_ : tmp_dev_).push_back(p);
+    } else {
+      if (slot) (void)(pinned ? hipHostFree(slot) : hipFree(slot));
+      slot = p;
+      cap = need;
+    }
+    *out = p;
+    return SF_OK;
+  }
+  std::unique_lock<std::mutex> lk_;
+  HostRes* r_ = nullptr;
+  HostRes* own_ = nullptr;
+  std::vector<void*> tmp_dev_, tmp_pin_;
+};
+
 // Chunk of input handled per pipeline stage: a whole number of blocks, about
 // 256 MiB.
 inline uint64_t stage_bytes(uint32_t bs) {
@@ -224,19 +329,18 @@ int index_pipelined(uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap, 
   if (nblocks == 0) return SF_OK;
   const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
   const uint64_t nstages = ceil_div(len, stage);
-  Streams st;
-  DevBuf ddata[2], ddig;
-  PinBuf pin[2], pdig;
-  for (int i = 0; i < 2; i++) {
-    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
-    SF_HIP(hipMalloc(&ddata[i].p, stage));
-    SF_HIP(hipHostMalloc(&pin[i].p, stage, hipHostMallocDefault));
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *pin[2], *ddig, *pdig;
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, stage, &ddata[i]);
+    if (rc == SF_OK) rc = res.pin(i, stage, &pin[i]);
   }
-  SF_HIP(hipMalloc(&ddig.p, nblocks * 20));
-  SF_HIP(hipHostMalloc(&pdig.p, nblocks * 20, hipHostMallocDefault));
-  hipEvent_t done[2] = {nullptr, nullptr};
-  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
-  int rc = SF_OK;
+  if (rc == SF_OK) rc = res.dev(2, nblocks * 20, &ddig);
+  if (rc == SF_OK) rc = res.pin(2, nblocks * 20, &pdig);
+  if (rc != SF_OK) return rc;
   for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const uint64_t off = k * stage;
@@ -244,22 +348,21 @@ int index_pipelined(uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap, 
     if (k >= 2) {
       if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
     }
-    rc = read(static_cast<uint8_t*>(pin[b].p), off, n);
+    rc = read(static_cast<uint8_t*>(pin[b]), off, n);
     if (rc != SF_OK) break;
-    if (hipMemcpyAsync(ddata[b].p, pin[b].p, n, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    if (hipMemcpyAsync(ddata[b], pin[b], n, hipMemcpyHostToDevice, st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
     const uint64_t first_blk = off / bs;
     const uint64_t nb = ceil_div(n, bs);
-    rc = launch_fixed(ddata[b].p, n, bs, nb, static_cast<uint8_t*>(ddig.p) + first_blk * 20, st.s[b]);
+    rc = launch_fixed(ddata[b], n, bs, nb, static_cast<uint8_t*>(ddig) + first_blk * 20, st[b]);
     if (rc != SF_OK) break;
-    if (hipEventRecord(done[b], st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    if (hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
   }
-  for (int i = 0; i < 2; i++) {
-    if (hipStreamSynchronize(st.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
-    (void)hipEventDestroy(done[i]);
-  }
+  for (int i = 0; i < 2; i++)
+    if (hipStreamSynchronize(st[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   if (rc != SF_OK) return rc;
-  SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
-  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
+  SF_HIP(hipMemcpyAsync(pdig, ddig, nblocks * 20, hipMemcpyDeviceToHost, st[0]));
+  SF_HIP(hipStreamSynchronize(st[0]));
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig);
   for (uint64_t i = 0; i < nblocks; i++) {
     out[i].offset = i * bs;
     out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
@@ -296,6 +399,18 @@ int sf_device_count(int* n) {
 }
 
 int sf_set_device(int device) { return hip_err(hipSetDevice(device)); }
+
+int sf_release_host_cache(void) {
+  for (int d = 0; d < kMaxDevices; d++) {
+    std::lock_guard<std::mutex> lk(g_res_mu[d]);  // waits for a call using the set
+    if (g_res[d]) {
+      g_res[d]->free_all();
+      delete g_res[d];
+      g_res[d] = nullptr;
+    }
+  }
+  return SF_OK;
+}
 
 int sf_index_device_fixed(const void* d_data, uint64_t len, uint32_t block_size, void* d_digests,
                           uint64_t cap_blocks, uint64_t* n_blocks, void* stream) {
@@ -656,27 +771,19 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
   };
   reg(0);
   if (regs[0].second != kLocked && regs[0].second != kPinned) return SF_ENOTSUP;
-  Streams st;
-  DevBuf ddata[2], ddig;
-  PinBuf pdig;
-  for (int i = 0; i < 2; i++) {
-    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
-    SF_HIP(hipMalloc(&ddata[i].p, stage));
-  }
-  SF_HIP(hipMalloc(&ddig.p, nblocks * 20));
-  SF_HIP(hipHostMalloc(&pdig.p, nblocks * 20, hipHostMallocDefault));
-  hipEvent_t done[2] = {nullptr, nullptr};
-  struct Evs {
-    hipEvent_t* e;
-    ~Evs() {
-      for (int i = 0; i < 2; i++)
-        if (e[i]) (void)hipEventDestroy(e[i]);
-    }
-  } evs{done};
-  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  PinBuf bounce;  // only if a region after the first cannot be registered
+  HostLease res;  // declared after unreg and bounce: its release waits for the streams first
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *ddig, *pdig;
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) rc = res.dev(i, stage, &ddata[i]);
+  if (rc == SF_OK) rc = res.dev(2, nblocks * 20, &ddig);
+  if (rc == SF_OK) rc = res.pin(2, nblocks * 20, &pdig);
+  if (rc != SF_OK) return rc;
   sf_host_sha1_stream bh;
   sf_host_sha1_begin(&bh);
-  const uint8_t* dg = static_cast<const uint8_t*>(pdig.p);
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig);
   auto rows = [&](uint64_t k) {  // rows + blocks_hash of stage k (its digests are on the host)
     const uint64_t b0 = k * stage / bs, b1 = std::min(nblocks, ceil_div((k + 1) * stage, bs));
     for (uint64_t i = b0; i < b1; i++) {
@@ -686,18 +793,16 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
     }
     if (blocks_hash) sf_host_sha1_update(&bh, dg + 20 * b0, (b1 - b0) * 20);
   };
-  PinBuf bounce;  // only if a region after the first cannot be registered
-  int rc = SF_OK;
   for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const uint64_t off = k * stage;
     const uint64_t n = std::min(stage, len - off);
     const uint64_t b0 = off / bs, nb = ceil_div(n, bs);
-    uint8_t* dd = static_cast<uint8_t*>(ddig.p) + b0 * 20;
+    uint8_t* dd = static_cast<uint8_t*>(ddig) + b0 * 20;
     const uint8_t* src = data + off;
     if (!serial && regs.back().second == kPageable) {  // region k is not page-locked: bounce
       for (int i = 0; i < 2; i++)
-        if (hipStreamSynchronize(st.s[i]) != hipSuccess) rc = SF_ENODEV;
+        if (hipStreamSynchronize(st[i]) != hipSuccess) rc = SF_ENODEV;
       if (rc != SF_OK) break;
       if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
       memcpy(bounce.p, src, n);
@@ -709,17 +814,17 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
     const uint64_t head = (serial || src != data + off || k == 0) ? 0 : std::min<uint64_t>(n, edge(k) - (uintptr_t)src);
     // stream b is in order: the copy into ddata[b] waits for the kernel of
     // stage k-2 that read it.
-    if ((head && hipMemcpyAsync(ddata[b].p, src, head, hipMemcpyHostToDevice, st.s[b]) != hipSuccess) ||
-        (n > head && hipMemcpyAsync(static_cast<uint8_t*>(ddata[b].p) + head, src + head, n - head,
-                                    hipMemcpyHostToDevice, st.s[b]) != hipSuccess)) {
+    if ((head && hipMemcpyAsync(ddata[b], src, head, hipMemcpyHostToDevice, st[b]) != hipSuccess) ||
+        (n > head && hipMemcpyAsync(static_cast<uint8_t*>(ddata[b]) + head, src + head, n - head,
+                                    hipMemcpyHostToDevice, st[b]) != hipSuccess)) {
       rc = SF_ENODEV;
       break;
     }
-    rc = launch_fixed(ddata[b].p, n, bs, nb, dd, st.s[b]);
+    rc = launch_fixed(ddata[b], n, bs, nb, dd, st[b]);
     if (rc != SF_OK) break;
     if (!serial) {
-      if (hipMemcpyAsync(static_cast<uint8_t*>(pdig.p) + b0 * 20, dd, nb * 20, hipMemcpyDeviceToHost, st.s[b]) != hipSuccess ||
-          hipEventRecord(done[b], st.s[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+      if (hipMemcpyAsync(static_cast<uint8_t*>(pdig) + b0 * 20, dd, nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+          hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
       if (k + 1 < nstages) reg(k + 1);
       if (k >= 1) {
         if (hipEventSynchronize(done[b ^ 1]) != hipSuccess) { rc = SF_ENODEV; break; }
@@ -728,10 +833,11 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
     }
   }
   for (int i = 0; i < 2; i++)
-    if (hipStreamSynchronize(st.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+    if (hipStreamSynchronize(st[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   if (rc != SF_OK) return rc;
   if (serial) {
-    SF_HIP(hipMemcpy(pdig.p, ddig.p, nblocks * 20, hipMemcpyDeviceToHost));
+    SF_HIP(hipMemcpyAsync(pdig, ddig, nblocks * 20, hipMemcpyDeviceToHost, st[0]));
+    SF_HIP(hipStreamSynchronize(st[0]));
     for (uint64_t k = 0; k < nstages; k++) rows(k);
   } else {
     rows(nstages - 1);

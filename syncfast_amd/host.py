@@ -37,6 +37,12 @@ def index_buffer(data, block_size: int) -> np.ndarray:
     return out[:n]
 
 
+def release_cache() -> None:
+    """Free the streams and buffers the host entry points keep between calls
+    (sf_release_host_cache)."""
+    check(lib().sf_release_host_cache(), "sf_release_host_cache")
+
+
 def index_file(path, block_size: int) -> Tuple[np.ndarray, bytes]:
     """Signatures of a file on disk + its blocks_hash."""
     size = os.path.getsize(path)

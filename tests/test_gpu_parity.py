@@ -242,6 +242,32 @@ def test_index_buffer_already_pinned(gpu, inplace_case):
     assert np.array_equal(rows["sha1"], want)
 
 
+def test_host_cache_reuse_release_and_threads(gpu, inplace_case):
+    # the per-device set kept between calls: a smaller call after a larger
+    # one, a release, and two threads at once (one takes the cached set, the
+    # other a private one) all give the oracle's rows
+    import threading
+    data, want = inplace_case
+    small = data[3:3 + (100 << 20) + 77]
+    want_small = oracle.index_fixed_mt(small, 4096, 8)  # its last block is short
+    assert np.array_equal(host.index_buffer(data[3:], 4096)["sha1"], want)
+    assert np.array_equal(host.index_buffer(small, 4096)["sha1"], want_small)
+    host.release_cache()
+    assert np.array_equal(host.index_buffer(small, 4096)["sha1"], want_small)
+    got = [None, None]
+
+    def run(i):
+        torch.cuda.set_device(gpu)
+        got[i] = host.index_buffer(data[3:] if i == 0 else small, 4096)["sha1"]
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert np.array_equal(got[0], want) and np.array_equal(got[1], want_small)
+
+
 @pytest.mark.parametrize("fail_at", ["", "1"])
 def test_index_file_inplace_multi_stage(gpu, inplace_case, fail_at, monkeypatch, tmp_path):
     # a page-cache-resident file of 2.4 stages: mapped, locked region by
