@@ -36,3 +36,19 @@ for mib in (64, 256, 1024):
         os.unlink(path)
     t = min(ts)
     print(f"sf_index_file   {mib:5d} MiB: {t * 1e3:8.2f} ms  {mib * MiB / t / 1e9:6.2f} GB/s", flush=True)
+# many files through one sf_index_files call: 8 MiB files, trees of 8..512
+with tempfile.TemporaryDirectory(dir=d) as td:
+    paths = []
+    for i in range(512):
+        p = os.path.join(td, f"f{i:04d}")
+        with open(p, "wb") as f:
+            f.write(b[i * 8 * MiB:(i + 1) * 8 * MiB].tobytes())
+        paths.append(p)
+    for nf in (8, 32, 128, 512):
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            host.index_files(paths[:nf], 4096)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        print(f"sf_index_files {nf:4d} x 8 MiB: {t * 1e3:8.2f} ms  {nf * 8 * MiB / t / 1e9:6.2f} GB/s", flush=True)

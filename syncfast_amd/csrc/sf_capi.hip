@@ -221,12 +221,16 @@ constexpr int kMaxDevices = 64;
 struct HostRes {
   hipStream_t s[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
-  void* dev[3] = {nullptr, nullptr, nullptr};  // stage 0, stage 1, digest table
-  uint64_t dev_cap[3] = {0, 0, 0};
-  void* pin[3] = {nullptr, nullptr, nullptr};  // stage 0, stage 1, digest table
-  uint64_t pin_cap[3] = {0, 0, 0};
+  // Slots (device and pinned alike): 0, 1 = the two stages; 2 = the digest
+  // table of one file; 3, 4 = the digest tables of sf_index_files' two
+  // stages; 5, 6 = their blocks_hash arrays.
+  static constexpr int kSlots = 7;
+  void* dev[kSlots] = {};
+  uint64_t dev_cap[kSlots] = {};
+  void* pin[kSlots] = {};
+  uint64_t pin_cap[kSlots] = {};
   void free_all() {
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < kSlots; i++) {
       if (dev[i]) (void)hipFree(dev[i]);
       if (pin[i]) (void)hipHostFree(pin[i]);
       dev[i] = pin[i] = nullptr;
@@ -1102,20 +1106,22 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     max_rows = std::max(max_rows, st.rows);
     max_files = std::max<uint64_t>(max_files, st.files.size());
   }
-  Streams sts;
-  DevBuf ddata[2], ddig[2], dfh[2];
-  PinBuf pin[2], pdig[2], pfh[2];
-  for (int i = 0; i < 2; i++) {
-    SF_HIP(hipStreamCreateWithFlags(&sts.s[i], hipStreamNonBlocking));
-    SF_HIP(hipMalloc(&ddata[i].p, max_bytes));
-    SF_HIP(hipMalloc(&ddig[i].p, max_rows * 20));
-    SF_HIP(hipMalloc(&dfh[i].p, max_files * 20));
-    SF_HIP(hipHostMalloc(&pin[i].p, std::min<uint64_t>(max_bytes, stage), hipHostMallocDefault));
-    SF_HIP(hipHostMalloc(&pdig[i].p, max_rows * 20, hipHostMallocDefault));
-    SF_HIP(hipHostMalloc(&pfh[i].p, max_files * 20, hipHostMallocDefault));
+  HostLease res;
+  hipStream_t* streams;
+  hipEvent_t* done;
+  rc = res.streams(streams, done);
+  struct Buf {
+    void* p;
+  } ddata[2], ddig[2], dfh[2], pin[2], pdig[2], pfh[2];
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, max_bytes, &ddata[i].p);
+    if (rc == SF_OK) rc = res.dev(3 + i, max_rows * 20, &ddig[i].p);
+    if (rc == SF_OK) rc = res.dev(5 + i, max_files * 20, &dfh[i].p);
+    if (rc == SF_OK) rc = res.pin(i, std::min<uint64_t>(max_bytes, stage), &pin[i].p);
+    if (rc == SF_OK) rc = res.pin(3 + i, max_rows * 20, &pdig[i].p);
+    if (rc == SF_OK) rc = res.pin(5 + i, max_files * 20, &pfh[i].p);
   }
-  hipEvent_t done[2] = {nullptr, nullptr};
-  for (int i = 0; i < 2; i++) SF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  if (rc != SF_OK) return rc;
   auto harvest = [&](size_t k) {
     const FileStage& st = stages[k];
     const int b = (int)(k & 1);
@@ -1148,7 +1154,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     map_stage(paths, st, size, maps[b], mptr);
     rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad, mptr);
     if (rc) break;
-    hipStream_t s = sts.s[b];
+    hipStream_t s = streams[b];
     // H2D: each mapped file from its mapping, every run of consecutive
     // pread files from the pinned stage in one copy.
     uint8_t* dd = static_cast<uint8_t*>(ddata[b].p);
@@ -1180,11 +1186,10 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     }
   }
   for (int i = 0; i < 2; i++)
-    if (hipStreamSynchronize(sts.s[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+    if (hipStreamSynchronize(streams[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   for (int i = 0; i < 2; i++) maps[i].release();  // every copy has completed
   if (rc == SF_OK)
     for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size(); k++) harvest(k);
-  for (int i = 0; i < 2; i++) (void)hipEventDestroy(done[i]);
   if (rc == SF_EIO && bad.load() >= 0) return fail((uint32_t)bad.load(), rc);
   return rc;
 }
