@@ -64,6 +64,24 @@ def test_argument_validation_without_device():
     assert L.sf_blocks_hash(None, 0, None) == _lib.SF_EINVAL
 
 
+def test_host_paths_without_device():
+    """Without a GPU the host-memory entry points fail cleanly: the in-place
+    route (>= 64 MiB) cannot page-lock, the staged route cannot set up its
+    streams, and the call returns SF_ENODEV; releasing the (empty) per-device
+    cache is a no-op."""
+    L = syncfast_amd.lib()
+    nd = ctypes.c_int(0)
+    if L.sf_device_count(ctypes.byref(nd)) == 0 and nd.value > 0:
+        pytest.skip("a device is visible")
+    n = ctypes.c_uint64(0)
+    data = np.zeros(64 << 20, np.uint8)
+    out = np.zeros((64 << 20) // 4096, host.SIG_DTYPE)
+    rc = L.sf_index_buffer(data.ctypes.data, data.size, 4096, out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)),
+                           out.size, ctypes.byref(n))
+    assert rc == _lib.SF_ENODEV and n.value == out.size
+    assert L.sf_release_host_cache() == 0
+
+
 def test_index_files_validation_without_device(tmp_path):
     """sf_index_files sizes every file and checks capacity before any read or
     device call: empty list, missing file (named by index), ENOSPC."""
