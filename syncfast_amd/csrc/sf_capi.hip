@@ -315,6 +315,14 @@ class HostLease {
   std::vector<void*> tmp_dev_, tmp_pin_;
 };
 
+// Reader threads of the pread routes (sf_index_file, sf_index_files).
+// SF_IO_THREADS overrides the default of 8 (A/B knob).
+inline unsigned io_threads() {
+  const char* e = getenv("SF_IO_THREADS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? (unsigned)std::min(v, 64) : 8u;
+}
+
 // Chunk of input handled per pipeline stage: a whole number of blocks, about
 // 256 MiB.
 inline uint64_t stage_bytes(uint32_t bs) {
@@ -909,7 +917,7 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   }
   // Each stage is read by several threads in parallel (one pread stream per
   // slice): one thread copies from the page cache at ~16 GB/s, below PCIe.
-  const unsigned nthreads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
   rc = index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
     auto read_slice = [&](uint64_t a, uint64_t b) {
       uint64_t got = a;
@@ -1032,7 +1040,7 @@ int read_stage(const char* const* paths, const FileStage& st, const std::vector<
     }
   };
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nthreads = (unsigned)std::min<size_t>(std::min(8u, hw), std::max<size_t>(1, items.size()));
+  const unsigned nthreads = (unsigned)std::min<size_t>(std::min(io_threads(), hw), std::max<size_t>(1, items.size()));
   std::vector<std::thread> pool;
   for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
   worker();
