@@ -323,6 +323,21 @@ inline unsigned io_threads() {
   return v > 0 ? (unsigned)std::min(v, 64) : 8u;
 }
 
+// Smallest host buffer / page-cache-resident file that sf_index_buffer /
+// sf_index_file copy in place (page-locked) instead of staging through the
+// pinned stages.  Per call, with the per-device set cached
+// (scripts/inplace_min_probe.py): a buffer gains in place from 1 MiB up
+// (7.6 vs 6.1 GB/s; 32 MiB: 45 vs 21); a file only from ~16 MiB (mapping and
+// locking page-cache pages loses to the 8-thread pread below 8 MiB: 4 MiB
+// 8.7 vs 10.3 GB/s; 32 MiB 24.3 vs 23.6).  SF_INPLACE_MIN_MIB overrides both
+// (A/B knob).
+inline uint64_t inplace_min_bytes(bool file) {
+  const char* e = getenv("SF_INPLACE_MIN_MIB");
+  const long v = e ? atol(e) : -1;
+  if (v >= 0) return (uint64_t)v << 20;
+  return file ? 16ull << 20 : 1ull << 20;
+}
+
 // Chunk of input handled per pipeline stage: a whole number of blocks, about
 // 256 MiB.
 inline uint64_t stage_bytes(uint32_t bs) {
@@ -866,7 +881,7 @@ int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_b
   // Large buffers: page-lock in place (no staging memcpy); SF_NO_HOSTREG=1
   // forces the staged path (A/B knob).
   const char* noreg = getenv("SF_NO_HOSTREG");
-  if (len >= (64ull << 20) && !(noreg && atoi(noreg))) {
+  if (len && len >= inplace_min_bytes(false) && !(noreg && atoi(noreg))) {
     rc = index_inplace(data, len, block_size, out, cap, n_out, nullptr);
     if (rc != SF_ENOTSUP) return rc;
   }
@@ -896,7 +911,7 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   // that is mostly not resident keeps the pread pipeline, which overlaps the
   // disk reads with the device.  SF_NO_MMAP=1 forces pread (A/B knob).
   const char* nomm = getenv("SF_NO_MMAP");
-  if (len >= (64ull << 20) && !(nomm && atoi(nomm))) {
+  if (len && len >= inplace_min_bytes(true) && !(nomm && atoi(nomm))) {
     void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
     if (m != MAP_FAILED) {
       const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);

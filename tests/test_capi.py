@@ -66,7 +66,7 @@ def test_argument_validation_without_device():
 
 def test_host_paths_without_device():
     """Without a GPU the host-memory entry points fail cleanly: the in-place
-    route (>= 64 MiB) cannot page-lock, the staged route cannot set up its
+    route (>= 1 MiB) cannot page-lock, the staged route cannot set up its
     streams, and the call returns SF_ENODEV; releasing the (empty) per-device
     cache is a no-op."""
     L = syncfast_amd.lib()

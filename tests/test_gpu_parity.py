@@ -188,7 +188,7 @@ def test_index_file_end_to_end(gpu):
 
 @pytest.mark.parametrize("no_mmap", ["0", "1"])
 def test_index_file_large_both_routes(gpu, no_mmap, monkeypatch):
-    # >= 64 MiB and in the page cache (just written): the mmap + hostRegister
+    # >= 16 MiB and in the page cache (just written): the mmap + hostRegister
     # route; SF_NO_MMAP=1 forces the pread pipeline.  Same rows either way.
     monkeypatch.setenv("SF_NO_MMAP", no_mmap)
     data = oracle.splitmix_bytes((96 << 20) + 4093, 95)
@@ -280,6 +280,22 @@ def test_index_file_inplace_multi_stage(gpu, inplace_case, fail_at, monkeypatch,
     rows, bh = host.index_file(str(path), 4096)
     assert np.array_equal(rows["sha1"], want)
     assert bh == oracle.blocks_hash(want)
+
+
+@pytest.mark.parametrize("min_mib", ["", "1024"])
+def test_small_buffer_and_file_routes(gpu, min_mib, monkeypatch, tmp_path):
+    # defaults: buffers >= 1 MiB and page-cache files >= 16 MiB in place;
+    # SF_INPLACE_MIN_MIB=1024 stages both through the pinned buffers
+    if min_mib:
+        monkeypatch.setenv("SF_INPLACE_MIN_MIB", min_mib)
+    for n, seed in [((2 << 20) + 13, 97), ((20 << 20) + 4095, 98)]:
+        data = oracle.splitmix_bytes(n + 5, seed)
+        _, _, want = oracle.index_fixed(data[5:], 4096)
+        assert np.array_equal(host.index_buffer(data[5:], 4096)["sha1"], want)
+        path = tmp_path / f"f{seed}.bin"
+        path.write_bytes(data[5:].tobytes())
+        rows, bh = host.index_file(str(path), 4096)
+        assert np.array_equal(rows["sha1"], want) and bh == oracle.blocks_hash(want)
 
 
 def test_block_digest_independent_of_neighbours(gpu):
