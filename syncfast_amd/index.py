@@ -29,6 +29,7 @@ import datetime as _dt
 import logging
 import os
 import sqlite3
+import stat
 from pathlib import Path, PurePath
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -111,6 +112,13 @@ def _mtime(path) -> _dt.datetime:
 
 
 # ----------------------------------------------------------------- chunkers
+
+def _seekable(f) -> bool:
+    """A regular file: the native routes map or pread it.  Anything else
+    File::open accepts (a FIFO, a character device) is streamed instead; the
+    C-ABI's sf_index_file needs a seekable file."""
+    return stat.S_ISREG(os.fstat(f.fileno()).st_mode)
+
 
 class FixedChunker:
     """Blocks of `block_size` bytes (last one shorter); no empty blocks."""
@@ -346,7 +354,10 @@ class Index:
             if up_to_date:
                 return
             if isinstance(self.chunker, FixedChunker):
-                rows_np, _ = host.index_file(path, self.chunker.block_size)
+                if _seekable(f):
+                    rows_np, _ = host.index_file(path, self.chunker.block_size)
+                else:  # a FIFO: stream it from this open, as File::open + read do
+                    rows_np = host.index_buffer(np.frombuffer(f.read(), np.uint8), self.chunker.block_size)
                 rows = host.rows_to_tuples(rows_np)
             else:
                 rows = signatures_of_bytes(f.read(), self.chunker)
@@ -397,8 +408,16 @@ class Index:
         bs = self.chunker.block_size
         pending = []  # (file_id, path) needing signatures
         for p, rel in todo:
-            with open(p, "rb"):  # same error as File::open on a vanished file
+            with open(p, "rb") as f:  # same error as File::open on a vanished file
                 file_id, up_to_date = self.add_file(rel, _mtime(p))
+                if not up_to_date and not _seekable(f):
+                    # a FIFO in the tree: read it from this open (a second
+                    # open would wait for another writer); rows like index_file
+                    rows = host.rows_to_tuples(host.index_buffer(np.frombuffer(f.read(), np.uint8), bs))
+                    self.add_blocks(file_id, rows)
+                    bh = self.compute_blocks_hash(file_id)
+                    self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
+                    continue
             if not up_to_date:
                 pending.append((file_id, p))
         if not pending:

@@ -158,6 +158,38 @@ def test_index_path_fixed_blocks(gpu, tmp_path, batch_bytes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("via", ["index_file", "index_path"])
+def test_fifo_is_streamed(gpu, tmp_path, via):
+    """The reference's index_file streams any path File::open accepts; a FIFO
+    (no size, no seek) gets the same rows as a regular file with its bytes."""
+    import threading
+    root = tmp_path / "tree"
+    root.mkdir()
+    fifo = root / "pipe"
+    os.mkfifo(fifo)
+    data = oracle.splitmix_bytes(3 * 4096 + 1234, 77)
+
+    def writer():
+        with open(fifo, "wb") as w:
+            w.write(data.tobytes())
+
+    th = threading.Thread(target=writer)
+    th.start()
+    idx = Index.open_in_memory(chunker=FixedChunker(4096))
+    if via == "index_file":
+        idx.index_file(fifo, PurePath("pipe"))
+    else:
+        idx.index_path(root)
+    th.join(timeout=30)
+    idx.commit()
+    fid, _, bh = idx.get_file("pipe")
+    offs, sizes, want = oracle.index_fixed(data, 4096)
+    got = idx.list_file_blocks(fid)
+    assert [(g[0].bytes, g[1], g[2]) for g in got] == [(bytes(w), int(o), int(s)) for w, o, s in zip(want, offs, sizes)]
+    assert bh.bytes == oracle.blocks_hash(want)
+
+
+@pytest.mark.gpu
 def test_boundary_chunker_random(gpu):
     rng = np.random.default_rng(5)
     data = oracle.splitmix_bytes(200_000, 77).tobytes()
