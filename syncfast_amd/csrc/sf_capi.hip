@@ -986,19 +986,30 @@ struct StageMaps {
   ~StageMaps() { release(); }
 };
 
-constexpr uint64_t kMapMinBytes = 64ull << 20;  // smaller files: pread (registering an 8 MiB file costs ~0.5 ms: slower than the 8-thread pread copy)
+// Files of a stage that are DMA'd from their page-locked mappings instead of
+// being read into the pinned stage: none by default.  With the per-device
+// cache, the 8-thread pread stage beats per-file registration at every size
+// measured (scripts/map_min_probe.py: 16 MiB files 40 vs 23 GB/s, 64 MiB 46
+// vs 33, 128 MiB 45 vs 34).  SF_MAP_MIN_MIB=n maps files >= n MiB (A/B knob).
+// Files larger than a stage still take sf_index_file's in-place route.
+inline uint64_t map_min_bytes() {
+  const char* e = getenv("SF_MAP_MIN_MIB");
+  const long v = e ? atol(e) : -1;
+  return v >= 0 ? (uint64_t)v << 20 : ~0ull;
+}
 
 // mapped[k] = the k-th file of the stage is mapped + registered (at ptrs[k]).
 void map_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, StageMaps& maps,
                std::vector<const uint8_t*>& ptrs) {
   ptrs.assign(st.files.size(), nullptr);
+  const uint64_t map_min = map_min_bytes();
   const char* nomm = getenv("SF_NO_MMAP");
   if (nomm && atoi(nomm)) return;
   const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
   std::vector<unsigned char> res;
   for (size_t k = 0; k < st.files.size(); k++) {
     const uint64_t n = size[st.files[k]];
-    if (n < kMapMinBytes) continue;
+    if (n < map_min) continue;
     const int fd = open(paths[st.files[k]], O_RDONLY);
     if (fd < 0) continue;  // the pread route reports the error
     struct stat sb;
@@ -1145,6 +1156,17 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     if (rc == SF_OK) rc = res.pin(5 + i, max_files * 20, &pfh[i].p);
   }
   if (rc != SF_OK) return rc;
+  // Per stage: each file's blocks_hash from a device chain (one lane per
+  // file, in the batch launch) while the runs are short; on the host (SHA-NI
+  // over the digests, in harvest) once the longest run would keep a lone
+  // chain lane busy past the stage's copy.  A chain costs ~1.1 us per 64 B of
+  // digests: 128 MiB files (640 KiB runs) took 11.6 ms per 256 MiB stage,
+  // against 4.7 ms of PCIe (scripts/map_min_probe.py).
+  constexpr uint64_t kDevChainMaxRun = 192u << 10;
+  std::vector<char> dev_bh(stages.size(), 1);
+  for (size_t k = 0; k < stages.size(); k++)
+    for (uint32_t f : stages[k].files)
+      if ((first_row[f + 1] - first_row[f]) * 20 > kDevChainMaxRun) dev_bh[k] = 0;
   auto harvest = [&](size_t k) {
     const FileStage& st = stages[k];
     const int b = (int)(k & 1);
@@ -1160,7 +1182,8 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
         o[i].size = (uint32_t)std::min<uint64_t>(bs, size[f] - i * bs);
         memcpy(o[i].sha1, dg + 20 * r, 20);
       }
-      memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
+      if (dev_bh[k]) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
+      else sf_host_sha1_impl(dg + 20 * (r - nb), nb * 20, blocks_hashes + 20ull * f, 0);
     }
   };
   std::atomic<int64_t> bad{-1};
@@ -1199,10 +1222,10 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     if (rc) break;
     uint64_t nb = 0;
     rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
-                               max_rows, dfh[b].p, nullptr, &nb, s);
+                               max_rows, dev_bh[k] ? dfh[b].p : nullptr, nullptr, &nb, s);
     if (rc) break;
     if ((nb && hipMemcpyAsync(pdig[b].p, ddig[b].p, nb * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        hipMemcpyAsync(pfh[b].p, dfh[b].p, st.files.size() * 20, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (dev_bh[k] && hipMemcpyAsync(pfh[b].p, dfh[b].p, st.files.size() * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipEventRecord(done[b], s) != hipSuccess) {
       rc = SF_ENODEV;
       break;
