@@ -98,6 +98,24 @@ def test_missing_blocks_and_temp_files():
 
 # ---- GPU: the hot path inside Index.index_file ----------------------------
 
+def test_seekable_routes_fifo_to_stream(tmp_path):
+    """Regular files take the native file routes; a FIFO is streamed from
+    its one open (Index.index_file / index_path)."""
+    import threading
+    from syncfast_amd.index import _seekable
+    reg = tmp_path / "r"
+    reg.write_bytes(b"x")
+    with open(reg, "rb") as f:
+        assert _seekable(f)
+    fifo = tmp_path / "p"
+    os.mkfifo(fifo)
+    th = threading.Thread(target=lambda: open(fifo, "wb").close())
+    th.start()
+    with open(fifo, "rb") as f:
+        assert not _seekable(f)
+    th.join(timeout=10)
+
+
 KAT_SIZES = [11579, 32768, 546]  # src/index.rs:771,778,785
 
 
