@@ -20,25 +20,33 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
   roofline      -- the SHA-1 kernel's algorithmic bytes / its average launch
                    time (HIP events on the launch stream) vs 8.0 TB/s HBM peak;
                    traffic = HBM bytes per launch from rocprofv3 PMC counters
-                   (profiles/, measured separately) or null;
+                   (profiles/traffic.json, measured separately on the SAME
+                   library build -- keyed by the .so's SHA-256 -- else null);
   cpu_baseline  -- the C oracle (single-threaded SHA-1 port of the
                    reference loop) on a bounded sample of the same bytes, rank 0
-                   at N=1 only.
+                   at N=1 only; cpu_baseline_shani the same tiling with the
+                   product's SHA-NI host SHA-1, on 1 core and on all cores;
+  config1       -- BASELINE configs[0] (the unmodified Rust CPU path): probed
+                   live (cargo / rustc on this host) and reported as not
+                   runnable when they are absent.
+
+Launch: --gpus N > 1 without torchrun (no WORLD_SIZE in the environment)
+starts the N rank processes itself -- torch.distributed.run as a CHILD
+process, before anything here touches the GPU -- and exits with its status;
+rank 0 asserts that the process group holds N ranks.
 """
 import argparse
+import hashlib
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-from syncfast_amd import device, host  # noqa: E402
-from syncfast_amd.shard import gather_digests, shard_range  # noqa: E402
 
 GiB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
@@ -90,7 +98,61 @@ def parse():
                         "configs 2 and 5 only); not the headline")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--check-launch", action="store_true",
+                   help="launcher check only (no GPU): every rank joins the process group (gloo), rank 0 "
+                        "prints the world size it saw and exits")
     return p.parse_args()
+
+
+def self_launch(a) -> int:
+    """--gpus N without a launcher: run this script under torch.distributed.run
+    as a child process (never an exec: the parent has not touched the GPU and
+    only waits), one rank per GPU, on a free local port."""
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: --gpus {a.gpus} without WORLD_SIZE: launching {a.gpus} ranks", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def check_launch(a, world, rank) -> None:
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    seen = torch.ones(1)
+    dist.all_reduce(seen)
+    assert dist.get_world_size() == world == a.gpus and int(seen.item()) == a.gpus, (world, a.gpus, seen)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item())}),
+              flush=True)
+    dist.destroy_process_group()
+
+
+def lib_sha256() -> str:
+    """SHA-256 of the HIP library this process runs (keys profiles/traffic.json)."""
+    from syncfast_amd._lib import LIB_PATH
+    h = hashlib.sha256()
+    with open(LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def config1_probe():
+    """BASELINE configs[0] needs the unmodified Rust indexer (cargo build of
+    /root/reference): probe for the toolchain on this host."""
+    tools = {t: shutil.which(t) for t in ("cargo", "rustc")}
+    cargo_home = os.path.isdir(os.path.expanduser("~/.cargo"))
+    runnable = all(tools.values())
+    return {"workload": "index a folder with one 64 MiB file, default CDC, unmodified Rust CPU path (BASELINE configs[0])",
+            "status": "runnable (not timed here)" if runnable else "reference CPU path not runnable",
+            "probe": {**{k: (v or "absent") for k, v in tools.items()}, "~/.cargo": cargo_home},
+            "note": None if runnable else "no Rust toolchain on this host; cpu_baseline times the C restatement "
+                                          "(scalar, stands in for the sha1 0.6 crate) and cpu_baseline_shani the "
+                                          "SHA-NI host code on the same fixed tiling instead"}
 
 
 def cpu_baseline(nbytes_total, bs, budget_s):
@@ -115,6 +177,26 @@ def cpu_baseline(nbytes_total, bs, budget_s):
                       f"oracle/sf_oracle.c SHA-1 (scalar C, no SHA-NI), 1 thread, SQLite excluded"}
 
 
+def cpu_baseline_shani(nbytes_total, bs, budget_s, threads):
+    """The same fixed tiling with the product's host SHA-1 (SHA-NI): the
+    strongest CPU number for this work, on `threads` cores."""
+    import oracle
+    piece = ((256 if threads > 1 else 64) << 20)
+    piece -= piece % bs
+    done, t_hash = 0, 0.0
+    while done < nbytes_total and t_hash < budget_s:
+        n = min(piece, nbytes_total - done)
+        buf = oracle.splitmix_bytes(n, SEED, done)
+        t0 = time.perf_counter()
+        oracle.index_fixed_shani(buf, bs, threads)
+        t_hash += time.perf_counter() - t0
+        done += n
+    return {"value": round(done / GiB / t_hash, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"first {done / GiB:.3f} GiB of the same stream, {bs}-B blocks, host SHA-1 with "
+                      f"{'SHA-NI' if oracle.has_shani() else 'scalar (no SHA-NI on this CPU)'} "
+                      f"(syncfast_amd/csrc/host_sha1.cpp via oracle/sf_baseline.cpp), {threads} thread(s)"}
+
+
 def cpu_baseline_all_cores(nbytes_total, bs, budget_s):
     """Same port on every host core this process may use (capped at 16, the
     GPU box's CPU share), 256 MiB pieces, bounded by the time budget."""
@@ -135,13 +217,30 @@ def cpu_baseline_all_cores(nbytes_total, bs, budget_s):
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(self_launch(a))  # before any torch.cuda / HIP call in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
+    if a.gpus != world:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % ndev)  # % only matters for single-GPU rehearsals
+    if a.check_launch:
+        return check_launch(a, world, rank)
+
+    import torch
+    import torch.distributed as dist
+    from syncfast_amd import device, host
+    from syncfast_amd.shard import gather_digests, shard_range
+
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    if ndev == 0:
+        raise SystemExit("bench.py needs a ROCm device (syncfast_amd has no CPU path)")
+    if a.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"rank {rank}: local rank {local} but only {ndev} GPU(s): RCCL needs one GPU per rank "
+                         f"(use --dist-backend gloo for a shared-GPU rehearsal)")
+    dev = torch.device("cuda", local % ndev)  # % only for gloo rehearsals on fewer GPUs than ranks
     torch.cuda.set_device(dev)
     distributed = world > 1
     if distributed:
@@ -149,6 +248,12 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(a.dist_backend)
+        # every rank joined and the communicator carries data: N ranks, N ones
+        ones = torch.ones(1, device=dev) if a.dist_backend == "nccl" else torch.ones(1)
+        dist.all_reduce(ones)
+        if dist.get_world_size() != a.gpus or int(ones.item()) != a.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks ({int(ones.item())} answered), "
+                             f"--gpus {a.gpus}")
 
     cfg = CONFIGS[a.config]
     bs = cfg["block"]
@@ -171,6 +276,7 @@ def main():
         flen = shard // cfg["files"]
         files = [(i * flen, flen) for i in range(cfg["files"])]
     fhash = torch.empty((len(files), 20), dtype=torch.uint8, device=dev) if files else None
+    status = torch.zeros(1, dtype=torch.int32, device=dev)  # staged batch: SF_ETIMEDOUT if a chain gave up
     if a.weak and files is not None:
         raise SystemExit("--weak applies to configs 2 and 5")
     weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)] if a.weak else None
@@ -203,7 +309,7 @@ def main():
                 last_hashes[0] = h
         else:
             device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
-                                      stream=stream)
+                                      stream=stream, status=status)
         if timed:
             ev[i][1].record(stream)
         if gather:
@@ -259,6 +365,8 @@ def main():
     dig = digs[(a.steps - 1) % nbuf]
     gathered = last_table[0]() if last_table[0] is not None else None
 
+    if int(status.item()) != 0:
+        raise SystemExit(f"staged batch reported status {int(status.item())} (SF_ETIMEDOUT: a blocks_hash chain gave up)")
     # Self-check (product host SHA-1): first and last block of this shard.
     d = dig.cpu().numpy()
     first = data[:bs].cpu().numpy()
@@ -295,19 +403,26 @@ def main():
     if weaks is not None:  # + 4 B weak sum written per block
         alg_bytes += nblk * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # PMC traffic of the same kernel on the same library build (else null:
+    # numbers from another build are stale).
     traffic = None
+    build = lib_sha256()
     try:
         with open(a.traffic_file) as f:
             tr = json.load(f)
         key = f"config{a.config}"
-        if key in tr and tr[key].get("shard_bytes") == shard and not a.weak:
-            traffic = tr[key]["hbm_bytes_per_launch"]
+        ent = tr.get(key, {})
+        if ent.get("shard_bytes") == shard and ent.get("lib_sha256") == build and not a.weak:
+            traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
-    cpu = cpu_all = None
+    cpu = cpu_all = cpu_ni = cpu_ni_all = None
     if not a.no_cpu_baseline and world == 1:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(shard, bs, a.cpu_seconds)
         cpu_all = cpu_baseline_all_cores(shard, bs, a.cpu_seconds / 4)
+        cpu_ni = cpu_baseline_shani(shard, bs, a.cpu_seconds / 4, 1)
+        cpu_ni_all = cpu_baseline_shani(shard, bs, a.cpu_seconds / 4, threads)
 
     line = {
         "metric": "GiB/s indexed (device-resident), %d KiB blocks" % (bs // 1024)
@@ -343,6 +458,10 @@ def main():
                      "the chip holds ~2.1 GHz under this load (DESIGN.md section 4)"},
         "cpu_baseline": cpu,
         "cpu_baseline_all_cores": cpu_all,
+        "cpu_baseline_shani": cpu_ni,
+        "cpu_baseline_shani_all_cores": cpu_ni_all,
+        "config1": config1_probe() if world == 1 else None,
+        "lib_sha256": build,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
     }

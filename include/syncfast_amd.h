@@ -48,6 +48,7 @@ extern "C" {
 #define SF_EINVAL (-22)  /* bad argument */
 #define SF_ENOSPC (-28)  /* output capacity too small; *n_out holds the need */
 #define SF_ERANGE (-34)  /* a block lies outside [0, len) */
+#define SF_ETIMEDOUT (-110) /* a device-side wait gave up; the affected blocks_hash values are invalid */
 
 /* One signature row: what index_file passes to add_block
  * (src/index.rs:636-642) and what FILE_BLOCK carries on the wire
@@ -115,11 +116,18 @@ int sf_index_device_blocks_weak(const void *d_data, uint64_t len, const uint64_t
  * file's blocks_hash (20 B per file, src/index.rs:661-682) computed on the
  * device.  first_block (host, n_files+1 entries, may be NULL) receives the
  * index of each file's first digest row; *n_blocks the total.  Asynchronous
- * on `stream` (ragged batches upload a small block table, stream-ordered). */
+ * on `stream` (ragged batches upload a small block table, stream-ordered).
+ * d_status (device int32, caller-initialised to 0, may be NULL): equal-size
+ * batches with d_file_hashes run ONE fused launch whose blocks_hash lanes
+ * wait (bounded) for the block digests they consume; if a wait gives up,
+ * those files' hashes are zeroed and *d_status is set to SF_ETIMEDOUT --
+ * the caller must check it before using d_file_hashes.  With d_status ==
+ * NULL the batch takes the non-waiting path (block kernel, then a chain
+ * kernel), which cannot time out. */
 int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *files,
                           uint32_t n_files, uint32_t block_size, void *d_digests,
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
-                          uint64_t *n_blocks, void *stream);
+                          uint64_t *n_blocks, int *d_status, void *stream);
 
 /* Per-file blocks_hash (src/index.rs:661-682) of a batch of equal-size files
  * already hashed into d_digests (n_files files x blocks rows, blocks a
@@ -178,9 +186,23 @@ int sf_index_buffer(const uint8_t *data, uint64_t len, uint32_t block_size,
 
 /* End to end from a file on disk (the reference's input, src/index.rs:615):
  * pread into pinned buffers, overlapped H2D + kernel, D2H.  Writes the
- * rows and the file's blocks_hash.  Blocking. */
+ * rows and the file's blocks_hash.  Blocking.  A path that cannot seek (FIFO,
+ * socket, character device) is read sequentially to EOF like File::open +
+ * read (src/index.rs:615,625); its input is consumed, so when the rows
+ * exceed cap the call returns SF_ENOSPC with *n_out = the need and the rows
+ * are lost -- use sf_index_fd for such inputs. */
 int sf_index_file(const char *path, uint32_t block_size, sf_block_sig *out, uint64_t cap,
                   uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
+/* Sequential input from an open file descriptor (pipe, FIFO, socket, or a
+ * file read from its current position), read to EOF: the rows of its fixed
+ * tiling, offsets from the first byte read, in a buffer the library
+ * allocates and grows (*rows; release it with sf_free_rows), and its
+ * blocks_hash.  Pinned double-buffered stages, each copied and hashed on
+ * the device while the next is read.  Does not close fd.  Blocking. */
+int sf_index_fd(int fd, uint32_t block_size, sf_block_sig **rows, uint64_t *n_out,
+                uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+void sf_free_rows(sf_block_sig *rows);
 
 /* Many files from disk: what index_path (src/index.rs:685-715) does by calling
  * index_file (src/index.rs:610-659) once per file, as ONE pipeline.  Fixed

@@ -27,7 +27,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libsf_oracle.so")
+_BASE_PATH = os.path.join(_HERE, "build", "libsf_baseline.so")
 _lib = None
+_base = None
 
 GAMMA = 0x9E3779B97F4A7C15
 MASK64 = (1 << 64) - 1
@@ -36,7 +38,8 @@ MASK64 = (1 << 64) - 1
 def build(force: bool = False) -> str:
     """Compile sf_oracle.c with gcc (no reference sources involved)."""
     src = os.path.join(_HERE, "sf_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    if (force or not os.path.exists(_LIB_PATH) or not os.path.exists(_BASE_PATH)
+            or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
@@ -64,6 +67,22 @@ def lib() -> ctypes.CDLL:
         L.sfo_adler_blocks.argtypes = [u8p, u8p, u8p, ctypes.c_uint64, u8p]
         _lib = L
     return _lib
+
+
+def baseline_lib() -> ctypes.CDLL:
+    """libsf_baseline.so: the SHA-NI CPU baseline (bench.py only)."""
+    global _base
+    if _base is None:
+        if not os.path.exists(_BASE_PATH):
+            build()
+        L = ctypes.CDLL(_BASE_PATH)
+        L.sfb_has_shani.argtypes = []
+        L.sfb_has_shani.restype = ctypes.c_int
+        L.sfb_index_fixed_shani.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                            ctypes.c_int]
+        L.sfb_index_fixed_shani.restype = ctypes.c_uint64
+        _base = L
+    return _base
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -102,6 +121,20 @@ def index_fixed_mt(data, block_size: int, threads: int) -> np.ndarray:
     dig = np.zeros((n, 20), np.uint8)
     lib().sfo_index_fixed_mt(_ptr(a), a.size, block_size, _ptr(dig), threads)
     return dig
+
+
+def index_fixed_shani(data, block_size: int, threads: int = 1) -> np.ndarray:
+    """Fixed tiling with the product's host SHA-1 (SHA-NI): the strongest CPU
+    baseline for bench.py, not a checker."""
+    a = _as_u8(data)
+    n = lib().sfo_num_blocks(a.size, block_size)
+    dig = np.zeros((n, 20), np.uint8)
+    baseline_lib().sfb_index_fixed_shani(_ptr(a), a.size, block_size, _ptr(dig), threads)
+    return dig
+
+
+def has_shani() -> bool:
+    return bool(baseline_lib().sfb_has_shani())
 
 
 def index_blocks(data, offsets, sizes) -> np.ndarray:

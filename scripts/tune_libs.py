@@ -68,17 +68,18 @@ def batch(libs, data, size, bs, s):
         f = L.sf_index_device_batch
         f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(FileDesc), ctypes.c_uint32, ctypes.c_uint32,
                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
-                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+                      ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_void_p]
         f.restype = ctypes.c_int
         fs.append(f)
         dig.append(torch.empty((n, 20), dtype=torch.uint8, device="cuda"))
         fh.append(torch.empty((nf, 20), dtype=torch.uint8, device="cuda"))
     nb = ctypes.c_uint64()
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")  # chain status (SF_ETIMEDOUT), checked at the end
     times = [[] for _ in libs]
 
     def call(i):
         assert fs[i](data.data_ptr(), size, files, nf, bs, dig[i].data_ptr(), n, fh[i].data_ptr(), None,
-                     ctypes.byref(nb), s.cuda_stream) == 0
+                     ctypes.byref(nb), st.data_ptr(), s.cuda_stream) == 0
     for _ in range(20):
         call(0)
     for r in range(int(os.environ.get("TUNE_ROUNDS", "6"))):
@@ -90,6 +91,7 @@ def batch(libs, data, size, bs, s):
             e1.record(s)
             torch.cuda.synchronize()
             times[i].append(e0.elapsed_time(e1) / 5)
+    assert int(st.item()) == 0, "a blocks_hash chain timed out"
     for i, p in enumerate(libs):
         assert torch.equal(dig[i], dig[0]) and torch.equal(fh[i], fh[0]), p
         med = statistics.median(times[i])

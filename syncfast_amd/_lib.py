@@ -21,6 +21,7 @@ SF_ENODEV = -19
 SF_EINVAL = -22
 SF_ENOSPC = -28
 SF_ERANGE = -34
+SF_ETIMEDOUT = -110
 
 HASH_DIGEST_LEN = 20
 MAX_BLOCK_SIZE = 32 << 20
@@ -30,7 +31,7 @@ EXPORTED = (
     "sf_version", "sf_strerror", "sf_device_count", "sf_set_device", "sf_release_host_cache",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
-    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_file", "sf_index_files",
+    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_file", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
 )
 
@@ -78,20 +79,23 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_index_device_fixed_weak.argtypes = [vp, u64, u32, vp, vp, u64, pu64, vp]
     L.sf_index_device_blocks_weak.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp, vp]
     L.sf_index_device_batch_chained.argtypes = [vp, u32, u64, u32, vp, ctypes.POINTER(ChainJob), u32, vp]
-    L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp]
+    L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp, vp]
     L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]
     L.sf_wire_file_blocks_fd.argtypes = [vp, u64, u32, u64, i32, pu64, vp]
     L.sf_index_buffer.argtypes = [vp, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
     L.sf_index_file.argtypes = [ctypes.c_char_p, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
+    L.sf_index_fd.argtypes = [i32, u32, ctypes.POINTER(ctypes.POINTER(BlockSig)), pu64, vp]
+    L.sf_free_rows.argtypes = [ctypes.POINTER(BlockSig)]
     L.sf_index_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), u32, u32, u64, ctypes.POINTER(BlockSig), u64,
                                  pu64, vp, pu64, ctypes.POINTER(ctypes.c_uint32)]
     L.sf_blocks_hash.argtypes = [vp, u64, vp]
     L.sf_blocks_hash_sigs.argtypes = [ctypes.POINTER(BlockSig), u64, vp]
     L.sf_sha1_host.argtypes = [vp, u64, vp]
     for name in EXPORTED:
-        if name not in ("sf_version", "sf_strerror"):
+        if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int
+    L.sf_free_rows.restype = None
 
 
 def lib() -> ctypes.CDLL:

@@ -144,8 +144,37 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
 // workgroups run the per-file chains while the others hash the blocks in S
 // column stages; only the last stage's chain work follows the last block.
 // Unstaged: the block kernel, then the stand-alone chain kernel.
+//
+// The chain waves wait on block waves, so the staged launch needs (a) block
+// workgroups to find free slots while every chain workgroup is resident and
+// (b) somewhere to report a chain that gave up.  (a): the chain workgroups
+// are kept to at most one per CU (a quarter of the staged kernel's 4
+// workgroups per CU); larger batches (> 256 x 256 files) take the unstaged
+// path, which never waits.  (b): d_status (device int32) receives
+// SF_ETIMEDOUT; with d_status == NULL the unstaged path is taken.
+// SF_CHAIN_SPIN_LIMIT (test knob) bounds the polls of each wait (default
+// 2^24, several seconds).
+inline unsigned device_cus() {
+  static std::atomic<int> cached{0};
+  int v = cached.load();
+  if (v > 0) return (unsigned)v;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess ||
+      hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) {
+    (void)hipGetLastError();
+    return 64;  // conservative (a quarter of MI355X's CUs)
+  }
+  cached.store(v);
+  return (unsigned)v;
+}
+
+inline uint32_t chain_spin_limit() {
+  const char* e = getenv("SF_CHAIN_SPIN_LIMIT");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 24);
+}
+
 int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
-                 uint8_t* fh, hipStream_t s) {
+                 uint8_t* fh, int* d_status, hipStream_t s) {
   int S = 1;
   const char* se = getenv("SF_STAGES");  // A/B knob; default up to 16 stages
   const int smax = se ? std::max(1, atoi(se)) : 16;
@@ -154,6 +183,7 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
       S = cand;
       break;
     }
+  if (!d_status || ceil_div(nfiles, 64 * sf::kWavesPerWG) > device_cus()) S = 1;
   if (S == 1) {
     int rc = launch_fixed(base, nbf * nfiles * (uint64_t)bs, bs, nbf * nfiles, dig, s);
     if (rc) return rc;
@@ -163,8 +193,8 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   }
   const uint64_t m = nbf / S;
   const sf::PadSchedule pad = pad_schedule(bs);
-  uint32_t* words = nullptr;  // [0, 32): stage counters, [32]: timeout word; 16-B padded block
-  const size_t wbytes = 48 * sizeof(uint32_t);
+  uint32_t* words = nullptr;  // [0, 32): stage counters
+  const size_t wbytes = 32 * sizeof(uint32_t);
   SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
 #ifdef SF_TUNING
@@ -178,7 +208,8 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   const unsigned chain_wgs = exp ? 0u : (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
   const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
-                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, exp == 2 ? nullptr : fh, words + 32);
+                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, exp == 2 ? nullptr : fh, d_status,
+                     chain_spin_limit());
   int rc = hip_err(hipGetLastError());
   (void)hipFreeAsync(words, s);
   return rc;
@@ -223,8 +254,8 @@ struct HostRes {
   hipEvent_t ev[2] = {nullptr, nullptr};
   // Slots (device and pinned alike): 0, 1 = the two stages; 2 = the digest
   // table of one file; 3, 4 = the digest tables of sf_index_files' two
-  // stages; 5, 6 = their blocks_hash arrays.
-  static constexpr int kSlots = 7;
+  // stages; 5, 6 = their blocks_hash arrays; 7 = their status words.
+  static constexpr int kSlots = 8;
   void* dev[kSlots] = {};
   uint64_t dev_cap[kSlots] = {};
   void* pin[kSlots] = {};
@@ -413,6 +444,7 @@ const char* sf_strerror(int code) {
     case SF_EINVAL: return "invalid argument";
     case SF_ENOSPC: return "output capacity too small";
     case SF_ERANGE: return "block outside the input";
+    case SF_ETIMEDOUT: return "device-side wait timed out (blocks_hash not computed)";
     default: return "unknown error";
   }
 }
@@ -479,7 +511,7 @@ int sf_index_device_blocks_weak(const void* d_data, uint64_t len, const uint64_t
 
 int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,
                           uint32_t block_size, void* d_digests, uint64_t cap_blocks, void* d_file_hashes,
-                          uint64_t* first_block, uint64_t* n_blocks, void* stream) {
+                          uint64_t* first_block, uint64_t* n_blocks, int* d_status, void* stream) {
   int rc = check_fixed_args(len, block_size);
   if (rc) return rc;
   if (n_files && !files) return SF_EINVAL;
@@ -515,7 +547,7 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
     if (!d_file_hashes)
       return launch_fixed(base, total * (uint64_t)block_size, block_size, total, d_digests, s);
     return batch_staged(base, files[0].len, block_size, n_files, nbf, static_cast<uint8_t*>(d_digests),
-                        static_cast<uint8_t*>(d_file_hashes), s);
+                        static_cast<uint8_t*>(d_file_hashes), d_status, s);
   }
 
   // Block table for the ragged case, file table for blocks_hash; one device
@@ -737,12 +769,17 @@ int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t s
 // k, and no page is registered twice.  A
 // region that cannot be registered after the first one switches the rest of
 // the stages to a pinned bounce buffer (memcpy, one stage at a time): slower,
-// same result.  Returns SF_ENOTSUP (nothing done) when the first
-// region cannot be registered, so the caller can take its staged route.
+// same result.  For a mapped file (fd >= 0) the bounce buffer is filled
+// with pread from the fd, never by touching the mapping: a region that cannot
+// be page-locked is typically one past a concurrent truncation, and reading
+// the mapping there would raise SIGBUS; pread returns short instead, and the
+// call fails with SF_EIO (the reference's read() would see the short file).
+// Returns SF_ENOTSUP (nothing done) when the first region cannot be
+// registered, so the caller can take its staged route.
 // SF_INPLACE_SERIAL=1 registers the whole range first and writes rows and
 // blocks_hash after the last stage (the previous form; A/B knob).
 static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
-                         uint64_t* n_out, uint8_t* blocks_hash) {
+                         uint64_t* n_out, uint8_t* blocks_hash, int fd = -1) {
   const uint64_t nblocks = ceil_div(len, bs);
   if (n_out) *n_out = nblocks;
   if (nblocks > cap) return SF_ENOSPC;
@@ -832,7 +869,18 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
         if (hipStreamSynchronize(st[i]) != hipSuccess) rc = SF_ENODEV;
       if (rc != SF_OK) break;
       if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
-      memcpy(bounce.p, src, n);
+      if (fd >= 0) {
+        uint8_t* d = static_cast<uint8_t*>(bounce.p);
+        for (uint64_t got = 0; got < n && rc == SF_OK;) {
+          const ssize_t r = pread(fd, d + got, n - got, (off_t)(off + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) rc = SF_EIO;  // error, or the file shrank under us
+          else got += (uint64_t)r;
+        }
+        if (rc != SF_OK) break;
+      } else {
+        memcpy(bounce.p, src, n);
+      }
       src = static_cast<const uint8_t*>(bounce.p);
     }
     // A copy must lie inside ONE registration: a stage that starts mid-page
@@ -873,6 +921,108 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
   return SF_OK;
 }
 
+// Sequential route (input that cannot seek: a pipe, FIFO, socket or
+// character device -- what index_file's File::open + read accepts,
+// src/index.rs:615,625): read() to EOF into two pinned stages of whole blocks
+// (the last one short); per stage, on alternating streams, H2D + block kernel
+// + D2H of the stage's digests.  While stage k is read, stage k-1 is on the
+// device; stage k-2's rows are appended (the row buffer grows, malloc'd) and
+// its digests folded into the streaming blocks_hash, in order.
+struct RowBuf {
+  sf_block_sig* p = nullptr;
+  uint64_t n = 0, cap = 0;
+  ~RowBuf() { free(p); }
+  bool grow(uint64_t need) {
+    if (need <= cap) return true;
+    uint64_t c = std::max<uint64_t>({need, 2 * cap, 1024});
+    void* q = realloc(p, c * sizeof(sf_block_sig));
+    if (!q) return false;
+    p = static_cast<sf_block_sig*>(q);
+    cap = c;
+    return true;
+  }
+  sf_block_sig* release() {
+    sf_block_sig* q = p;
+    p = nullptr;
+    n = cap = 0;
+    return q;
+  }
+};
+
+static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash) {
+  const char* se = getenv("SF_STREAM_STAGE_MIB");  // test knob: small stages exercise the pipeline
+  const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) << 20 : (256ull << 20);
+  const uint64_t stage = std::max<uint64_t>(1, want / bs) * bs;
+  const uint64_t sblocks = stage / bs;
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *pin[2], *ddig[2], *pdig[2];
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, stage, &ddata[i]);
+    if (rc == SF_OK) rc = res.pin(i, stage, &pin[i]);
+    if (rc == SF_OK) rc = res.dev(3 + i, sblocks * 20, &ddig[i]);
+    if (rc == SF_OK) rc = res.pin(3 + i, sblocks * 20, &pdig[i]);
+  }
+  if (rc != SF_OK) return rc;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  uint64_t bytes_of[2] = {0, 0}, first_of[2] = {0, 0};
+  bool busy[2] = {false, false};
+  auto harvest = [&](int b) {
+    if (hipEventSynchronize(done[b]) != hipSuccess) return SF_ENODEV;
+    busy[b] = false;
+    const uint64_t nb = ceil_div(bytes_of[b], bs);
+    if (!rows.grow(rows.n + nb)) return SF_ENOMEM;
+    const uint8_t* dg = static_cast<const uint8_t*>(pdig[b]);
+    for (uint64_t i = 0; i < nb; i++) {
+      sf_block_sig& r = rows.p[rows.n + i];
+      r.offset = (first_of[b] + i) * bs;
+      r.size = (uint32_t)std::min<uint64_t>(bs, bytes_of[b] - i * bs);
+      memcpy(r.sha1, dg + 20 * i, 20);
+    }
+    rows.n += nb;
+    if (blocks_hash) sf_host_sha1_update(&bh, dg, nb * 20);
+    return SF_OK;
+  };
+  uint64_t total = 0;
+  bool eof = false;
+  for (uint64_t k = 0; !eof && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (busy[b] && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (stage k-1 is still later in order)
+    uint8_t* dst = static_cast<uint8_t*>(pin[b]);
+    uint64_t n = 0;
+    while (n < stage) {
+      const ssize_t r = read(fd, dst + n, stage - n);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) { rc = SF_EIO; break; }
+      if (r == 0) { eof = true; break; }
+      n += (uint64_t)r;
+    }
+    if (rc != SF_OK || n == 0) break;
+    const uint64_t nb = ceil_div(n, bs);
+    bytes_of[b] = n;
+    first_of[b] = total / bs;  // every earlier stage was whole blocks
+    total += n;
+    if (hipMemcpyAsync(ddata[b], dst, n, hipMemcpyHostToDevice, st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    if ((rc = launch_fixed(ddata[b], n, bs, nb, ddig[b], st[b])) != SF_OK) break;
+    if (hipMemcpyAsync(pdig[b], ddig[b], nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    busy[b] = true;
+  }
+  // the (at most two) stages still in flight, in file order
+  int order[2] = {0, 1};
+  if (busy[0] && busy[1] && first_of[1] < first_of[0]) std::swap(order[0], order[1]);
+  for (int b : order)
+    if (busy[b]) {
+      const int r = harvest(b);
+      if (rc == SF_OK) rc = r;
+    }
+  if (rc == SF_OK && blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
+  return rc;
+}
+
 int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
   int rc = check_fixed_args(len, block_size);
@@ -898,6 +1048,24 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   if (!path) return SF_EINVAL;
   const int fd = open(path, O_RDONLY);
   if (fd < 0) return SF_EIO;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || S_ISDIR(sb.st_mode)) { close(fd); return SF_EIO; }
+  if (!S_ISREG(sb.st_mode)) {
+    // Not seekable (FIFO, socket, character device): the sequential route.
+    // The input is consumed, so with too small a cap the rows are lost and
+    // SF_ENOSPC reports the need (sf_index_fd has no cap to miss).
+    RowBuf rows;
+    uint8_t bh[20];
+    rc = index_stream(fd, block_size, rows, bh);
+    close(fd);
+    if (rc != SF_OK) return rc;
+    if (n_out) *n_out = rows.n;
+    if (rows.n > cap) return SF_ENOSPC;
+    if (rows.n && !out) return SF_EINVAL;
+    if (rows.n) memcpy(out, rows.p, rows.n * sizeof(sf_block_sig));
+    if (blocks_hash) memcpy(blocks_hash, bh, 20);
+    return SF_OK;
+  }
   const off_t end = lseek(fd, 0, SEEK_END);
   if (end < 0) { close(fd); return SF_EIO; }
   const uint64_t len = (uint64_t)end;
@@ -920,7 +1088,7 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
       if (mincore(m, len, res.data()) == 0)
         for (unsigned char r : res) resident += r & 1u;
       if (resident * 10 >= res.size() * 9) {
-        rc = index_inplace(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out, blocks_hash);
+        rc = index_inplace(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out, blocks_hash, fd);
         if (rc != SF_ENOTSUP) {
           munmap(m, len);
           close(fd);
@@ -958,6 +1126,22 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
   return rc;
 }
+
+int sf_index_fd(int fd, uint32_t block_size, sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[20]) {
+  if (rows) *rows = nullptr;
+  if (n_out) *n_out = 0;
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (fd < 0 || !rows || !n_out) return SF_EINVAL;
+  RowBuf rb;
+  rc = index_stream(fd, block_size, rb, blocks_hash);
+  if (rc != SF_OK) return rc;
+  *n_out = rb.n;
+  *rows = rb.release();
+  return SF_OK;
+}
+
+void sf_free_rows(sf_block_sig* rows) { free(rows); }
 
 // ---- sf_index_files: many files, one pipeline ----------------------------
 
@@ -1146,7 +1330,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
   rc = res.streams(streams, done);
   struct Buf {
     void* p;
-  } ddata[2], ddig[2], dfh[2], pin[2], pdig[2], pfh[2];
+  } ddata[2], ddig[2], dfh[2], pin[2], pdig[2], pfh[2], dstat, pstat;
   for (int i = 0; i < 2 && rc == SF_OK; i++) {
     rc = res.dev(i, max_bytes, &ddata[i].p);
     if (rc == SF_OK) rc = res.dev(3 + i, max_rows * 20, &ddig[i].p);
@@ -1155,7 +1339,11 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     if (rc == SF_OK) rc = res.pin(3 + i, max_rows * 20, &pdig[i].p);
     if (rc == SF_OK) rc = res.pin(5 + i, max_files * 20, &pfh[i].p);
   }
+  if (rc == SF_OK) rc = res.dev(7, 2 * 16, &dstat.p);  // one int32 status per stage buffer, 16 B apart
+  if (rc == SF_OK) rc = res.pin(7, 2 * 16, &pstat.p);
   if (rc != SF_OK) return rc;
+  auto stat_dev = [&](int b) { return reinterpret_cast<int*>(static_cast<uint8_t*>(dstat.p) + 16 * b); };
+  auto stat_host = [&](int b) { return *reinterpret_cast<volatile int*>(static_cast<uint8_t*>(pstat.p) + 16 * b); };
   // Per stage: each file's blocks_hash from a device chain (one lane per
   // file, in the batch launch) while the runs are short; on the host (SHA-NI
   // over the digests, in harvest) once the longest run would keep a lone
@@ -1167,9 +1355,10 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
   for (size_t k = 0; k < stages.size(); k++)
     for (uint32_t f : stages[k].files)
       if ((first_row[f + 1] - first_row[f]) * 20 > kDevChainMaxRun) dev_bh[k] = 0;
-  auto harvest = [&](size_t k) {
+  auto harvest = [&](size_t k) {  // SF_OK, or the stage's device status (SF_ETIMEDOUT)
     const FileStage& st = stages[k];
     const int b = (int)(k & 1);
+    if (dev_bh[k] && stat_host(b) != SF_OK) return stat_host(b);
     const uint8_t* dg = static_cast<const uint8_t*>(pdig[b].p);
     const uint8_t* fh = static_cast<const uint8_t*>(pfh[b].p);
     uint64_t r = 0;
@@ -1185,6 +1374,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
       if (dev_bh[k]) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
       else sf_host_sha1_impl(dg + 20 * (r - nb), nb * 20, blocks_hashes + 20ull * f, 0);
     }
+    return SF_OK;
   };
   std::atomic<int64_t> bad{-1};
   StageMaps maps[2];
@@ -1194,7 +1384,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     const FileStage& st = stages[k];
     if (k >= 2) {
       if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
-      harvest(k - 2);
+      if ((rc = harvest(k - 2)) != SF_OK) break;
     }
     maps[b].release();  // stage k-2's copies are done (its event was waited for above)
     map_stage(paths, st, size, maps[b], mptr);
@@ -1221,11 +1411,15 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     }
     if (rc) break;
     uint64_t nb = 0;
+    if (dev_bh[k] && hipMemsetAsync(stat_dev(b), 0, sizeof(int), s) != hipSuccess) { rc = SF_ENODEV; break; }
     rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
-                               max_rows, dev_bh[k] ? dfh[b].p : nullptr, nullptr, &nb, s);
+                               max_rows, dev_bh[k] ? dfh[b].p : nullptr, nullptr, &nb,
+                               dev_bh[k] ? stat_dev(b) : nullptr, s);
     if (rc) break;
     if ((nb && hipMemcpyAsync(pdig[b].p, ddig[b].p, nb * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         (dev_bh[k] && hipMemcpyAsync(pfh[b].p, dfh[b].p, st.files.size() * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (dev_bh[k] && hipMemcpyAsync(static_cast<uint8_t*>(pstat.p) + 16 * b, stat_dev(b), sizeof(int),
+                                     hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipEventRecord(done[b], s) != hipSuccess) {
       rc = SF_ENODEV;
       break;
@@ -1235,7 +1429,8 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     if (hipStreamSynchronize(streams[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   for (int i = 0; i < 2; i++) maps[i].release();  // every copy has completed
   if (rc == SF_OK)
-    for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size(); k++) harvest(k);
+    for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size() && rc == SF_OK; k++)
+      rc = harvest(k);
   if (rc == SF_EIO && bad.load() >= 0) return fail((uint32_t)bad.load(), rc);
   return rc;
 }

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/syncfast_amd.h"
 #include "sha1_device.hpp"
 
 namespace sf {
@@ -375,13 +376,17 @@ __device__ __forceinline__ void sha1_stream_range(Sha1& st, const uint4* __restr
 // over its run of run_len digest bytes, consumed in S slices of mb bytes (a
 // multiple of 64).  With stage_done, slice k is read only after
 // stage_done[k] == waves_per_stage: ONE lane polls ONE word (relaxed, agent
-// scope, s_sleep, bounded), then an agent-scope acquire (MI355X guide,
-// Guideline 16).  A poll that gives up stores an all-zero hash and sets
-// *timeout (never expected: the producers never wait).
+// scope, s_sleep, at most spin_limit + 1 polls), then an agent-scope acquire
+// (MI355X guide, Guideline 16).  A poll that gives up stores an all-zero hash
+// and sets *status = SF_ETIMEDOUT, which the host reads back and returns (the
+// reference never yields a hash it did not compute, src/index.rs:661-682).
+// Never expected: the producers never wait, and the host keeps the chain
+// workgroups below the resident capacity (batch_staged).
 __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t f,
                                            bool valid, uint32_t run_len, uint32_t S, uint32_t mb,
                                            const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
-                                           uint8_t* __restrict__ out, uint32_t* __restrict__ timeout) {
+                                           uint8_t* __restrict__ out, int* __restrict__ status,
+                                           uint32_t spin_limit) {
   const int lane = threadIdx.x & 63;
   Sha1 st;
   st.init();
@@ -394,14 +399,14 @@ __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uin
       if (lane == 0) {
         for (uint32_t spins = 0;; ++spins) {
           seen = __hip_atomic_load(stage_done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (seen >= waves_per_stage || spins > (1u << 24)) break;
+          if (seen >= waves_per_stage || spins >= spin_limit) break;
           __builtin_amdgcn_s_sleep(8);
         }
       }
       seen = __builtin_amdgcn_readfirstlane(seen);
       if (seen < waves_per_stage) {
         ok = false;
-        if (lane == 0) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(status, SF_ETIMEDOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -432,7 +437,7 @@ __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
                   uint8_t* __restrict__ out) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr);
+  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr, 0);
 }
 
 // Deep-prefetch form of sha1_stream_range for chains that run beside a
@@ -652,7 +657,7 @@ __global__ void __launch_bounds__(kThreads, SF_STAGED_WPE)
 sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
                    uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
                    uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
-                   uint32_t* __restrict__ timeout) {
+                   int* __restrict__ status, uint32_t spin_limit) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -661,7 +666,7 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
     __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
     const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + lane;
     chain_wave(digests, out_stride * 20, f, f < rows, (uint32_t)(cols * 20), (uint32_t)(cols / m),
-               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, timeout);
+               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, status, spin_limit);
     return;
   }
   const uint64_t nblocks = rows * cols;

@@ -156,11 +156,18 @@ def index_device_blocks_weak(data: torch.Tensor, offsets: torch.Tensor, sizes: t
 
 def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], block_size: int,
                        file_hashes: bool = True, out: Optional[torch.Tensor] = None,
-                       hashes_out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None):
+                       hashes_out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
+                       status: Optional[torch.Tensor] = None):
     """Many files inside one HBM buffer.
 
     ``files`` = [(offset, length), ...].  Returns (digests uint8[n,20],
-    first_block int64[n_files+1], file_hashes uint8[n_files,20] or None)."""
+    first_block int64[n_files+1], file_hashes uint8[n_files,20] or None).
+
+    The per-file blocks_hash lanes of an equal-size batch wait (bounded) for
+    the digests they consume; a wait that gives up is reported as
+    SF_ETIMEDOUT.  With ``status`` (int32[1] on the device, zeroed by the
+    caller) the call stays asynchronous and the caller checks it; without,
+    the call synchronises the stream and raises SfError(SF_ETIMEDOUT)."""
     _require_device(data, "data", torch.uint8)
     nf = len(files)
     descs = (FileDesc * max(nf, 1))()
@@ -180,12 +187,23 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
             raise ValueError("hashes_out too small")
     first = np.zeros(nf + 1, np.uint64)
     nb = ctypes.c_uint64(0)
+    own_status = status is None and fh is not None
+    if own_status:
+        status = torch.zeros(1, dtype=torch.int32, device=data.device)
+    elif status is not None:
+        _require_device(status, "status", torch.int32)
     with torch.cuda.device(data.device):
         check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs, nf,
                                           block_size, dig.data_ptr() if total else None, dig.numel() // 20,
                                           fh.data_ptr() if fh is not None else None,
-                                          first.ctypes.data, ctypes.byref(nb), _stream_ptr(data, stream)),
+                                          first.ctypes.data, ctypes.byref(nb),
+                                          status.data_ptr() if status is not None else None,
+                                          _stream_ptr(data, stream)),
               "sf_index_device_batch")
+    if own_status:
+        code = int(status.item())
+        if code != 0:
+            raise SfError(code, "sf_index_device_batch")
     return dig, first.astype(np.int64), fh
 
 

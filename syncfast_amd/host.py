@@ -44,16 +44,41 @@ def release_cache() -> None:
 
 
 def index_file(path, block_size: int) -> Tuple[np.ndarray, bytes]:
-    """Signatures of a file on disk + its blocks_hash."""
+    """Signatures of a file on disk + its blocks_hash.  A regular file that
+    grows between the sizing stat and the call (SF_ENOSPC with the new need)
+    is indexed again with room for it, as index_files does."""
     size = os.path.getsize(path)
     n = (size + block_size - 1) // block_size if size else 0
-    out = np.zeros(max(n, 1), SIG_DTYPE)
     nout = ctypes.c_uint64(0)
     bh = (ctypes.c_uint8 * 20)()
-    check(lib().sf_index_file(os.fsencode(path), block_size, out.ctypes.data_as(ctypes.POINTER(BlockSig)),
-                              n, ctypes.byref(nout), bh),
-          "sf_index_file")
+    for _attempt in range(4):
+        out = np.zeros(max(n, 1), SIG_DTYPE)
+        rc = lib().sf_index_file(os.fsencode(path), block_size, out.ctypes.data_as(ctypes.POINTER(BlockSig)),
+                                 n, ctypes.byref(nout), bh)
+        if rc == SF_ENOSPC and nout.value > n:
+            n = nout.value
+            continue
+        break
+    check(rc, "sf_index_file")
     return out[:nout.value], bytes(bh)
+
+
+def index_fd(fd: int, block_size: int) -> Tuple[np.ndarray, bytes]:
+    """Signatures of everything readable from an open descriptor (a pipe, a
+    FIFO, ...) to EOF + its blocks_hash (sf_index_fd: sequential route, rows
+    in a library-grown buffer)."""
+    rows = ctypes.POINTER(BlockSig)()
+    nout = ctypes.c_uint64(0)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_fd(int(fd), block_size, ctypes.byref(rows), ctypes.byref(nout), bh), "sf_index_fd")
+    try:
+        n = nout.value
+        out = np.zeros(n, SIG_DTYPE)
+        if n:
+            ctypes.memmove(out.ctypes.data, rows, n * SIG_DTYPE.itemsize)
+    finally:
+        lib().sf_free_rows(rows)
+    return out, bytes(bh)
 
 
 def index_files(paths: Sequence, block_size: int, stage_bytes: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

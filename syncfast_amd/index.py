@@ -17,6 +17,17 @@ ZPAQ chunker (src/index.rs:622-625), whose recurrence is not available here
 SHA-1, the rows, ``blocks_hash`` and every query are bit-identical to the
 reference for the same boundaries.
 
+Timestamps.  ``files.modified`` is a ``DateTime<Utc>`` (``timestamp.DateTimeUtc``):
+taken from the open file's metadata with nanosecond precision
+(src/index.rs:616-619), written as chrono's RFC 3339 text and compared as a
+parsed value in the mtime gate (src/index.rs:183) -- see timestamp.py (parity
+with rusqlite's exact writer is unpinned).
+
+Walk order.  ``index_path`` visits directory entries in ``os.listdir`` order,
+which is readdir(3) order -- the order Rust's ``read_dir`` yields
+(src/index.rs:698) -- so ``file_id``s are assigned as the reference would on
+the same filesystem.
+
 Quirks kept on purpose: ``index_file`` leaves ``files.size`` NULL (the
 reference never sets it there, so ``list_files`` reports 0, src/index.rs:
 376-377); ``compute_blocks_hash`` hashes the digests in the order SQLite
@@ -25,7 +36,6 @@ returns them for ``WHERE file_id = ?`` with no ORDER BY (src/index.rs:663-
 """
 from __future__ import annotations
 
-import datetime as _dt
 import logging
 import os
 import sqlite3
@@ -37,6 +47,7 @@ import numpy as np
 
 from . import host
 from .digest import HashDigest
+from .timestamp import DateTimeUtc
 
 log = logging.getLogger("syncfast_amd.index")
 
@@ -101,22 +112,25 @@ def _name_str(name) -> str:
     return s
 
 
-def _ts(dt: _dt.datetime) -> str:
-    """DateTime<Utc> as text (RFC 3339, UTC)."""
-    return dt.astimezone(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%f+00:00")
+def _mtime(f) -> DateTimeUtc:
+    """``file.metadata()?.modified()?.into()`` (src/index.rs:616-619): the open
+    file's mtime, to the nanosecond."""
+    return DateTimeUtc.from_ns(os.fstat(f.fileno()).st_mtime_ns)
 
 
-def _mtime(path) -> _dt.datetime:
-    st = os.stat(path)
-    return _dt.datetime.fromtimestamp(st.st_mtime_ns / 1e9, tz=_dt.timezone.utc)
+def _now() -> DateTimeUtc:
+    """``chrono::Utc::now()`` (src/index.rs:265)."""
+    import time
+    return DateTimeUtc.from_ns(time.time_ns())
 
 
 # ----------------------------------------------------------------- chunkers
 
 def _seekable(f) -> bool:
     """A regular file: the native routes map or pread it.  Anything else
-    File::open accepts (a FIFO, a character device) is streamed instead; the
-    C-ABI's sf_index_file needs a seekable file."""
+    File::open accepts (a FIFO, a character device) is read sequentially from
+    the open descriptor (sf_index_fd): a second open of a FIFO would wait for
+    another writer."""
     return stat.S_ISREG(os.fstat(f.fileno()).st_mode)
 
 
@@ -209,18 +223,19 @@ class Index:
             "WHERE blocks.hash = ? AND blocks.present = 1;", (hash.to_sql(),)).fetchone()
         return (PurePath(row[0]), int(row[1]), int(row[2])) if row else None
 
-    def get_file(self, name) -> Optional[Tuple[int, str, Optional[HashDigest]]]:
+    def get_file(self, name) -> Optional[Tuple[int, DateTimeUtc, Optional[HashDigest]]]:
         row = self.db.execute(
             "SELECT file_id, modified, blocks_hash FROM files WHERE name = ? AND temporary = 0;",
             (_name_str(name),)).fetchone()
         if not row:
             return None
-        return int(row[0]), row[1], HashDigest.from_sql(row[2]) if row[2] is not None else None
+        return (int(row[0]), DateTimeUtc.from_sql(row[1]),
+                HashDigest.from_sql(row[2]) if row[2] is not None else None)
 
-    def get_temp_file(self, name) -> Optional[Tuple[int, str]]:
+    def get_temp_file(self, name) -> Optional[Tuple[int, DateTimeUtc]]:
         row = self.db.execute("SELECT file_id, modified FROM files WHERE name = ? AND temporary = 1;",
                               (_name_str(temp_name(name)),)).fetchone()
-        return (int(row[0]), row[1]) if row else None
+        return (int(row[0]), DateTimeUtc.from_sql(row[1])) if row else None
 
     def get_file_name(self, file_id: int) -> Optional[PurePath]:
         row = self.db.execute("SELECT name FROM files WHERE file_id = ?;", (file_id,)).fetchone()
@@ -229,7 +244,7 @@ class Index:
     def list_files(self):
         rows = self.db.execute(
             "SELECT file_id, name, modified, size, blocks_hash FROM files WHERE temporary = 0;").fetchall()
-        return [(int(r[0]), PurePath(r[1]), r[2], int(r[3] or 0),
+        return [(int(r[0]), PurePath(r[1]), DateTimeUtc.from_sql(r[2]), int(r[3] or 0),
                  HashDigest.from_sql(r[4]) if r[4] is not None else None) for r in rows]
 
     def list_file_blocks(self, file_id: int) -> List[Tuple[HashDigest, int, int]]:
@@ -255,14 +270,17 @@ class Index:
         return [(int(r[0]), PurePath(r[1]), int(r[2]), int(r[3])) for r in rows]
 
     # -- mutations (src/index.rs:176-408, 433-451, 591-607)
-    def add_file(self, name, modified: _dt.datetime) -> Tuple[int, bool]:
-        """(file_id, up_to_date): the mtime gate of src/index.rs:176-218."""
+    def add_file(self, name, modified) -> Tuple[int, bool]:
+        """(file_id, up_to_date): the mtime gate of src/index.rs:176-218.
+        ``modified``: DateTimeUtc, an aware datetime, or ns since the epoch;
+        compared with the stored value as an instant (src/index.rs:183)."""
         self.begin()
-        ts = _ts(modified)
+        m = DateTimeUtc.coerce(modified)
+        ts = m.to_sql()
         cur = self.get_file(name)
         if cur is not None:
             file_id, old_modified, _ = cur
-            if old_modified != ts:
+            if old_modified != m:
                 log.info("Resetting file %s, modified", name)
                 self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
                 self.db.execute("UPDATE files SET modified = ?, size = NULL, blocks_hash = NULL, temporary = 0 "
@@ -273,9 +291,9 @@ class Index:
         c = self.db.execute("INSERT INTO files(name, modified, temporary) VALUES(?, ?, 0);", (_name_str(name), ts))
         return int(c.lastrowid), False
 
-    def add_file_overwrite(self, name, modified: _dt.datetime) -> int:
+    def add_file_overwrite(self, name, modified) -> int:
         self.begin()
-        ts = _ts(modified)
+        ts = DateTimeUtc.coerce(modified).to_sql()
         cur = self.get_file(name)
         if cur is not None:
             file_id = cur[0]
@@ -288,7 +306,7 @@ class Index:
 
     def add_temp_file(self, name) -> int:
         self.begin()
-        ts = _ts(_dt.datetime.now(_dt.timezone.utc))
+        ts = _now().to_sql()
         tname = _name_str(temp_name(name))
         row = self.db.execute("SELECT file_id FROM files WHERE name = ? AND temporary = 0;", (tname,)).fetchone()
         if row is not None:
@@ -350,14 +368,14 @@ class Index:
     def index_file(self, path, name) -> None:
         """Cut a file into blocks and add them to the index."""
         with open(path, "rb") as f:  # File::open first: same error on a missing file
-            file_id, up_to_date = self.add_file(name, _mtime(path))
+            file_id, up_to_date = self.add_file(name, _mtime(f))
             if up_to_date:
                 return
             if isinstance(self.chunker, FixedChunker):
                 if _seekable(f):
                     rows_np, _ = host.index_file(path, self.chunker.block_size)
-                else:  # a FIFO: stream it from this open, as File::open + read do
-                    rows_np = host.index_buffer(np.frombuffer(f.read(), np.uint8), self.chunker.block_size)
+                else:  # a FIFO: read sequentially from this open, as File::open + read do
+                    rows_np, _ = host.index_fd(f.fileno(), self.chunker.block_size)
                 rows = host.rows_to_tuples(rows_np)
             else:
                 rows = signatures_of_bytes(f.read(), self.chunker)
@@ -390,7 +408,7 @@ class Index:
         p = root / rel
         if p.is_dir():
             log.info("Indexing directory %s (%s)", rel, p)
-            for entry in sorted(os.listdir(p)):
+            for entry in os.listdir(p):  # readdir order, as read_dir (src/index.rs:698)
                 if entry == INDEX_FILE_NAME:
                     continue
                 self._index_path_rec(root, rel / entry, todo)
@@ -409,11 +427,11 @@ class Index:
         pending = []  # (file_id, path) needing signatures
         for p, rel in todo:
             with open(p, "rb") as f:  # same error as File::open on a vanished file
-                file_id, up_to_date = self.add_file(rel, _mtime(p))
+                file_id, up_to_date = self.add_file(rel, _mtime(f))
                 if not up_to_date and not _seekable(f):
                     # a FIFO in the tree: read it from this open (a second
                     # open would wait for another writer); rows like index_file
-                    rows = host.rows_to_tuples(host.index_buffer(np.frombuffer(f.read(), np.uint8), bs))
+                    rows = host.rows_to_tuples(host.index_fd(f.fileno(), bs)[0])
                     self.add_blocks(file_id, rows)
                     bh = self.compute_blocks_hash(file_id)
                     self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))

@@ -2,9 +2,14 @@
 
 configs[1]: 8 GiB in 4 KiB blocks -- every one of the 2^21 digests compared
 with the multi-threaded C oracle on the host (bit-exact, plus blocks_hash).
-configs[4]: 32 GiB in 64 KiB blocks -- size-independent properties: a
-random sample of blocks vs the oracle, the last block, idempotence of a second
-launch, and the chunked-vs-whole checksum of checksums."""
+configs[4]: 32 GiB in 64 KiB blocks -- every one of the 2^19 digests vs the
+oracle, the bytes and digests streamed back in 4 GiB pieces; plus a fast
+sampled variant (size-independent properties: a random sample of blocks, the
+last block, idempotence of a second launch, chunked-vs-whole checksum of
+checksums).
+configs[3] (one rank's share): a 32 GiB shard at 4 KiB blocks indexed as N =
+2, 4 and 8 shard_range pieces on one device, concatenated, equals the whole
+launch, whose every digest is checked against the oracle in 4 GiB pieces."""
 import os
 
 import numpy as np
@@ -45,6 +50,50 @@ def test_config2_8gib_4k_every_digest(gpu):
     dt = device.index_device_blocks(data_t, torch.from_numpy(offs).to(gpu),
                                     torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
     assert np.array_equal(dt, oracle.index_blocks(host_bytes, offs, sizes))
+
+
+def _check_streamed(data, dig, bs, piece=4 * GiB):
+    """Every digest of `dig` (uint8[n, 20], host) against the oracle over the
+    device bytes, brought back piece by piece (host RAM stays ~2 pieces)."""
+    n = data.numel()
+    piece -= piece % bs
+    for off in range(0, n, piece):
+        ln = min(piece, n - off)
+        host_bytes = data[off:off + ln].cpu().numpy()
+        want = oracle.index_fixed_mt(host_bytes, bs, _threads())
+        got = dig[off // bs: off // bs + want.shape[0]]
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"piece at {off}: {bad.size} digests differ, first at block {off // bs + bad[:5]}"
+        del host_bytes, want
+
+
+def test_config5_32gib_64k_every_digest(gpu):
+    # configs[4] at full size: all 2^19 digests vs the multi-threaded oracle
+    n, bs = 32 * GiB, 65536
+    data = device.splitmix_tensor(n, 0x5EED0004, gpu)
+    dig = device.index_device(data, bs).cpu().numpy()
+    assert dig.shape == (n // bs, 20)
+    _check_streamed(data, dig, bs)
+
+
+def test_config4_32gib_4k_shard_pieces_every_digest(gpu):
+    # configs[3]: one GPU's 32 GiB shard of the 256 GiB file.  The shard
+    # split N ways with shard_range (the multi-GPU layout) and the pieces'
+    # tables concatenated in rank order must equal the whole launch (the
+    # file -> shards -> table-in-order invariant of src/index.rs:629-656);
+    # then every digest of the whole launch vs the oracle.
+    from syncfast_amd.shard import shard_range
+    n, bs = 32 * GiB, 4096
+    data = device.splitmix_tensor(n, 0x5EED0003, gpu)
+    whole = device.index_device(data, bs)
+    for world in (2, 4, 8):
+        parts = []
+        for r in range(world):
+            s, ln = shard_range(n, bs, world, r)
+            parts.append(device.index_device(data[s:s + ln], bs))
+        assert torch.equal(torch.cat(parts), whole), world
+        del parts
+    _check_streamed(data, whole.cpu().numpy(), bs)
 
 
 def test_config5_32gib_64k_properties(gpu):

@@ -1,0 +1,150 @@
+"""GPU: failure paths of the C-ABI report errors instead of wrong results.
+
+- The fused many-file launch (sha1_staged_kernel): its blocks_hash lanes wait
+  (bounded) for block digests; a wait that gives up must surface as
+  SF_ETIMEDOUT, never as an all-zero blocks_hash with rc = 0 (the reference
+  never yields a hash it did not compute, src/index.rs:661-682).  Forced with
+  SF_CHAIN_SPIN_LIMIT=0 (one poll per wait; test knob).
+- Batches too wide for the fused launch's chain workgroups to stay below the
+  resident capacity, and callers without a status word, take the non-waiting
+  path: correct hashes even with the spin limit at 0.
+- A file truncated while indexed (in-place route, bounce stages): no SIGBUS,
+  an error or a complete result.
+- index_file sized from a stale stat retries with the need (SF_ENOSPC)."""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from syncfast_amd import device, host
+from syncfast_amd._lib import SF_ETIMEDOUT, FileDesc, SfError, lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _equal_batch(gpu, nfiles, nbf, bs, seed):
+    data = oracle.splitmix_bytes(nfiles * nbf * bs, seed)
+    t = torch.from_numpy(data).to(gpu)
+    files = [(i * nbf * bs, nbf * bs) for i in range(nfiles)]
+    return data, t, files
+
+
+def test_staged_chain_timeout_is_an_error(gpu, monkeypatch):
+    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    _, t, files = _equal_batch(gpu, 64, 1024, 4096, 501)  # 256 MiB: stage 0 cannot be done at the first poll
+    with pytest.raises(SfError) as e:
+        device.index_device_batch(t, files, 4096)
+    assert e.value.code == SF_ETIMEDOUT
+    # the asynchronous form: the caller's status word carries it
+    st = torch.zeros(1, dtype=torch.int32, device=gpu)
+    device.index_device_batch(t, files, 4096, status=st)
+    assert int(st.item()) == SF_ETIMEDOUT
+
+
+def test_staged_default_spin_limit_is_green(gpu):
+    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 502)
+    st = torch.zeros(1, dtype=torch.int32, device=gpu)
+    dig, _, fh = device.index_device_batch(t, files, 4096, status=st)
+    assert int(st.item()) == 0
+    want = oracle.index_fixed_mt(data, 4096, 8)
+    assert np.array_equal(dig.cpu().numpy(), want)
+    assert bytes(fh.cpu().numpy()[63]) == oracle.blocks_hash(want[63 * 1024:])
+
+
+def test_index_files_reports_chain_timeout(gpu, monkeypatch, tmp_path):
+    # sf_index_files reads each stage's device status back: SF_ETIMEDOUT
+    # from the blocks_hash lanes of a stage fails the call
+    paths = []
+    for i in range(32):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(oracle.splitmix_bytes(8 << 20, 600 + i).tobytes())
+        paths.append(str(p))
+    rows, first, fh = host.index_files(paths, 4096)  # green first
+    want = oracle.index_fixed(np.fromfile(paths[5], np.uint8), 4096)[2]
+    assert bytes(fh[5]) == oracle.blocks_hash(want)
+    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    with pytest.raises(SfError) as e:
+        host.index_files(paths, 4096)
+    assert e.value.code == SF_ETIMEDOUT
+
+
+def test_null_status_takes_nonwaiting_path(gpu, monkeypatch):
+    # no status word: the batch runs block kernel + chain kernel (no waits),
+    # so even a zero spin limit gives the right hashes
+    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    nfiles, nbf, bs = 64, 1024, 4096
+    data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 503)
+    descs = (FileDesc * nfiles)(*[FileDesc(o, ln) for o, ln in files])
+    dig = torch.empty((nfiles * nbf, 20), dtype=torch.uint8, device=gpu)
+    fh = torch.empty((nfiles, 20), dtype=torch.uint8, device=gpu)
+    nb = ctypes.c_uint64()
+    rc = lib().sf_index_device_batch(t.data_ptr(), t.numel(), descs, nfiles, bs, dig.data_ptr(), nfiles * nbf,
+                                     fh.data_ptr(), None, ctypes.byref(nb), None,
+                                     torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    want = oracle.index_fixed_mt(data, bs, 8)
+    fhn = fh.cpu().numpy()
+    assert np.array_equal(dig.cpu().numpy(), want)
+    for i in (0, 31, 63):
+        assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
+
+
+def test_wide_batch_keeps_chains_below_residency(gpu, monkeypatch):
+    # 70,000 equal files: more chain workgroups (274) than CUs (256) -> the
+    # non-waiting path; with the spin limit at 0 a fused launch would time out
+    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    nfiles, nbf, bs = 70_000, 128, 64
+    data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 504)
+    dig, _, fh = device.index_device_batch(t, files, bs)
+    want = oracle.index_fixed_mt(data, bs, 8)
+    assert np.array_equal(dig.cpu().numpy(), want)
+    fhn = fh.cpu().numpy()
+    per = want.reshape(nfiles, nbf, 20)
+    for i in list(range(0, nfiles, 997)) + [nfiles - 1]:
+        assert bytes(fhn[i]) == oracle.blocks_hash(per[i]), i
+
+
+def test_truncated_during_inplace_route_no_sigbus(gpu, monkeypatch, tmp_path):
+    # every region after the first goes through the bounce buffer
+    # (SF_INPLACE_FAIL_AT=1), which now preads from the fd; a concurrent
+    # truncation gives SF_EIO or a complete, correct result -- never SIGBUS
+    monkeypatch.setenv("SF_INPLACE_FAIL_AT", "1")
+    monkeypatch.setenv("SF_INPLACE_MIN_MIB", "1")
+    size, bs = 768 << 20, 4096
+    data = oracle.splitmix_bytes(size, 505)
+    p = tmp_path / "shrinking"
+    outcomes = set()
+    for k in range(3):
+        data.tofile(p)
+        with open(p, "rb") as f:  # warm the page cache: the in-place route needs it resident
+            while f.read(64 << 20):
+                pass
+        cut = threading.Timer(0.002 * (k + 1), lambda: os.truncate(p, 3 << 20))
+        cut.start()
+        try:
+            rows, bh = host.index_file(p, bs)
+            outcomes.add("ok")
+            # completed before the cut (or the cut landed after every read)
+            got = np.stack([r["sha1"] for r in rows[:4]])
+            assert np.array_equal(got, oracle.index_fixed(data[:4 * bs], bs)[2])
+        except SfError as e:
+            outcomes.add(e.code)
+        finally:
+            cut.join()
+    assert outcomes <= {"ok", -5}, outcomes
+
+
+def test_index_file_retries_when_the_file_grew(gpu, monkeypatch, tmp_path):
+    p = tmp_path / "grows"
+    data = oracle.splitmix_bytes(5 * 4096 + 7, 506)
+    data.tofile(p)
+    real = os.path.getsize
+    monkeypatch.setattr(host.os.path, "getsize", lambda path: real(path) - 3 * 4096)  # a stale, smaller size
+    rows, bh = host.index_file(p, 4096)
+    offs, sizes, want = oracle.index_fixed(data, 4096)
+    assert len(rows) == 6 and np.array_equal(np.stack([r["sha1"] for r in rows]), want)
+    assert bh == oracle.blocks_hash(want)

@@ -216,3 +216,30 @@ def test_boundary_chunker_random(gpu):
     from syncfast_amd.index import signatures_of_bytes
     rows = signatures_of_bytes(data, BoundaryChunker(lambda d: sizes))
     assert [r[2] for r in rows] == oracle.py_index_blocks(data, [r[0] for r in rows], sizes)
+
+
+def test_walk_visits_entries_in_readdir_order(tmp_path):
+    # src/index.rs:698 iterates read_dir() as the filesystem yields it (no
+    # sort); os.listdir is the same readdir(3) order, so file_ids follow it
+    root = tmp_path / "w"
+    (root / "sub").mkdir(parents=True)
+    for n in ["zeta", "alpha", "Mid", "b10", "b9", ".hidden"]:
+        (root / n).write_bytes(b"x")
+        (root / "sub" / n).write_bytes(b"y")
+    (root / ".syncfast.idx").write_bytes(b"")
+    todo = []
+    Index.open_in_memory()._index_path_rec(root, PurePath(""), todo)
+
+    def expect(rel):
+        out = []
+        for e in os.listdir(root / rel):
+            if e == ".syncfast.idx":
+                continue
+            if (root / rel / e).is_dir():
+                out += expect(rel / e)
+            else:
+                out.append(rel / e)
+        return out
+
+    assert [str(r) for _p, r in todo] == [str(r) for r in expect(PurePath(""))]
+    assert len(todo) == 12
