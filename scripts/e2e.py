@@ -54,14 +54,17 @@ def main():
         f.write(data.tobytes())
         path = f.name
     try:
-        for i, env in enumerate([{}, {}, {"SF_INPLACE_SERIAL": "1"}, {}, {"SF_INPLACE_SERIAL": "1"}]):
+        # default = pread pipeline (stages read by 8 threads, rows + blocks_hash
+        # per stage); SF_FILE_INPLACE=1 = the opt-in mapped + page-locked route
+        inpl = {"SF_FILE_INPLACE": "1"}
+        for i, env in enumerate([{}, {}, inpl, {}, inpl, {}, inpl]):
             os.environ.update(env)
             t0 = time.perf_counter()
             rows, bh = host.index_file(path, 4096)
             t = time.perf_counter() - t0
             for k in env:
                 del os.environ[k]
-            what = "cold-ish" if i == 0 else "page cache, " + ("serial" if env else "overlapped")
+            what = "cold-ish" if i == 0 else "page cache, " + ("in place (opt-in)" if env else "pread pipeline")
             print(f"sf_index_file {n / GiB:.0f} GiB ({what}), incl. blocks_hash:", rate(n, t), flush=True)
     finally:
         os.unlink(path)

@@ -921,38 +921,27 @@ static int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_bloc
   return SF_OK;
 }
 
-// Sequential route (input that cannot seek: a pipe, FIFO, socket or
-// character device -- what index_file's File::open + read accepts,
-// src/index.rs:615,625): read() to EOF into two pinned stages of whole blocks
-// (the last one short); per stage, on alternating streams, H2D + block kernel
-// + D2H of the stage's digests.  While stage k is read, stage k-1 is on the
-// device; stage k-2's rows are appended (the row buffer grows, malloc'd) and
-// its digests folded into the streaming blocks_hash, in order.
-struct RowBuf {
-  sf_block_sig* p = nullptr;
-  uint64_t n = 0, cap = 0;
-  ~RowBuf() { free(p); }
-  bool grow(uint64_t need) {
-    if (need <= cap) return true;
-    uint64_t c = std::max<uint64_t>({need, 2 * cap, 1024});
-    void* q = realloc(p, c * sizeof(sf_block_sig));
-    if (!q) return false;
-    p = static_cast<sf_block_sig*>(q);
-    cap = c;
-    return true;
-  }
-  sf_block_sig* release() {
-    sf_block_sig* q = p;
-    p = nullptr;
-    n = cap = 0;
-    return q;
-  }
-};
+}  // extern "C"
 
-static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash) {
+namespace {
+
+// Staged file pipeline (sf_index_file's pread route and the sequential
+// route of sf_index_fd): two pinned stages of whole blocks (the last one
+// short).  `fill(dst, off, cap, &n, &eof)` puts the next input bytes into a
+// pinned stage; per stage, on alternating streams, H2D + block kernel + D2H of
+// the stage's digests.  While stage k is being filled, stage k-1 is on the
+// device and stage k-2's rows are emitted (`emit(first_block, n_blocks,
+// digests, stage_bytes)`) and its digests folded into the streaming
+// blocks_hash (src/index.rs:661-682), in order.  No device memory maps or
+// registers the caller's file: the host only ever reads it with read/pread.
+inline uint64_t file_stage_bytes(uint32_t bs) {
   const char* se = getenv("SF_STREAM_STAGE_MIB");  // test knob: small stages exercise the pipeline
   const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) << 20 : (256ull << 20);
-  const uint64_t stage = std::max<uint64_t>(1, want / bs) * bs;
+  return std::max<uint64_t>(1, want / bs) * bs;
+}
+
+template <typename FillFn, typename EmitFn>
+int staged_pipeline(uint32_t bs, uint64_t stage, FillFn fill, EmitFn emit, uint8_t* blocks_hash) {
   const uint64_t sblocks = stage / bs;
   HostLease res;
   hipStream_t* st;
@@ -974,15 +963,9 @@ static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash)
     if (hipEventSynchronize(done[b]) != hipSuccess) return SF_ENODEV;
     busy[b] = false;
     const uint64_t nb = ceil_div(bytes_of[b], bs);
-    if (!rows.grow(rows.n + nb)) return SF_ENOMEM;
     const uint8_t* dg = static_cast<const uint8_t*>(pdig[b]);
-    for (uint64_t i = 0; i < nb; i++) {
-      sf_block_sig& r = rows.p[rows.n + i];
-      r.offset = (first_of[b] + i) * bs;
-      r.size = (uint32_t)std::min<uint64_t>(bs, bytes_of[b] - i * bs);
-      memcpy(r.sha1, dg + 20 * i, 20);
-    }
-    rows.n += nb;
+    const int r = emit(first_of[b], nb, dg, bytes_of[b]);
+    if (r != SF_OK) return r;
     if (blocks_hash) sf_host_sha1_update(&bh, dg, nb * 20);
     return SF_OK;
   };
@@ -990,17 +973,10 @@ static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash)
   bool eof = false;
   for (uint64_t k = 0; !eof && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
-    if (busy[b] && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (stage k-1 is still later in order)
+    if (busy[b] && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (stage k-1 is later in file order)
     uint8_t* dst = static_cast<uint8_t*>(pin[b]);
     uint64_t n = 0;
-    while (n < stage) {
-      const ssize_t r = read(fd, dst + n, stage - n);
-      if (r < 0 && errno == EINTR) continue;
-      if (r < 0) { rc = SF_EIO; break; }
-      if (r == 0) { eof = true; break; }
-      n += (uint64_t)r;
-    }
-    if (rc != SF_OK || n == 0) break;
+    if ((rc = fill(dst, total, stage, &n, &eof)) != SF_OK || n == 0) break;
     const uint64_t nb = ceil_div(n, bs);
     bytes_of[b] = n;
     first_of[b] = total / bs;  // every earlier stage was whole blocks
@@ -1022,6 +998,101 @@ static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash)
   if (rc == SF_OK && blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
   return rc;
 }
+
+// Rows in a growing malloc'd buffer (sf_index_fd; the sequential route of
+// sf_index_file).
+struct RowBuf {
+  sf_block_sig* p = nullptr;
+  uint64_t n = 0, cap = 0;
+  ~RowBuf() { free(p); }
+  bool grow(uint64_t need) {
+    if (need <= cap) return true;
+    uint64_t c = std::max<uint64_t>({need, 2 * cap, 1024});
+    void* q = realloc(p, c * sizeof(sf_block_sig));
+    if (!q) return false;
+    p = static_cast<sf_block_sig*>(q);
+    cap = c;
+    return true;
+  }
+  sf_block_sig* release() {
+    sf_block_sig* q = p;
+    p = nullptr;
+    n = cap = 0;
+    return q;
+  }
+};
+
+inline void write_rows(sf_block_sig* o, uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes, uint32_t bs) {
+  for (uint64_t i = 0; i < nb; i++) {
+    o[i].offset = (first + i) * bs;
+    o[i].size = (uint32_t)std::min<uint64_t>(bs, bytes - i * bs);
+    memcpy(o[i].sha1, dg + 20 * i, 20);
+  }
+}
+
+// Sequential route (input that cannot seek: a pipe, FIFO, socket or
+// character device -- what index_file's File::open + read accepts,
+// src/index.rs:615,625): read() to EOF.
+static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash) {
+  auto fill = [&](uint8_t* dst, uint64_t, uint64_t cap, uint64_t* n, bool* eof) {
+    *n = 0;
+    while (*n < cap) {
+      const ssize_t r = read(fd, dst + *n, cap - *n);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) return SF_EIO;
+      if (r == 0) { *eof = true; break; }
+      *n += (uint64_t)r;
+    }
+    return SF_OK;
+  };
+  auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
+    if (!rows.grow(rows.n + nb)) return SF_ENOMEM;
+    write_rows(rows.p + rows.n, first, nb, dg, bytes, bs);
+    rows.n += nb;
+    return SF_OK;
+  };
+  return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
+}
+
+// Regular file of known length: each stage is read by several threads in
+// parallel (one pread stream per slice; one thread copies from the page
+// cache at ~16 GB/s, below PCIe).  A short read (the file shrank) is SF_EIO.
+static int index_file_pread(int fd, uint64_t len, uint32_t bs, sf_block_sig* out, uint8_t* blocks_hash) {
+  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
+  auto fill = [&](uint8_t* dst, uint64_t off, uint64_t cap, uint64_t* nout, bool* eof) {
+    const uint64_t n = std::min(cap, len - off);
+    *nout = n;
+    *eof = off + n >= len;
+    auto read_slice = [&](uint64_t a, uint64_t b) {
+      for (uint64_t got = a; got < b;) {
+        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return SF_EIO;
+        got += (uint64_t)r;
+      }
+      return SF_OK;
+    };
+    const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
+    std::vector<std::thread> pool;
+    std::vector<int> rcs(nthreads, SF_OK);
+    for (unsigned t = 1; t < nthreads && t * slice < n; t++)
+      pool.emplace_back([&, t] { rcs[t] = read_slice(t * slice, std::min(n, (t + 1) * slice)); });
+    rcs[0] = read_slice(0, std::min(n, slice));
+    for (auto& th : pool) th.join();
+    for (int r : rcs)
+      if (r) return r;
+    return SF_OK;
+  };
+  auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
+    write_rows(out + first, first, nb, dg, bytes, bs);
+    return SF_OK;
+  };
+  return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
+}
+
+}  // namespace
+
+extern "C" {
 
 int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
@@ -1073,13 +1144,17 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   if (n_out) *n_out = nb;
   if (nb > cap) { close(fd); return SF_ENOSPC; }
   if (nb && !out) { close(fd); return SF_EINVAL; }
-  // A large file already in the page cache: map it and page-lock the mapping
-  // in place (hipHostRegister), so the DMA engine reads the page-cache pages
-  // directly -- no pread copy (the in-place path of sf_index_buffer).  A file
-  // that is mostly not resident keeps the pread pipeline, which overlaps the
-  // disk reads with the device.  SF_NO_MMAP=1 forces pread (A/B knob).
-  const char* nomm = getenv("SF_NO_MMAP");
-  if (len && len >= inplace_min_bytes(true) && !(nomm && atoi(nomm))) {
+  // Opt-in (SF_FILE_INPLACE=1): a large file already in the page cache is
+  // mapped and the mapping page-locked in place (hipHostRegister), so the DMA
+  // engine reads the page-cache pages directly -- no pread copy (the in-place
+  // path of sf_index_buffer).  Not the default: a registered file mapping is
+  // a GPU userptr, and a concurrent truncation of the file invalidates it
+  // under the in-flight copies -- measured on MI355X, the process's queues
+  // then never resume and the call hangs (tests/test_gpu_robustness.py).  The
+  // default pread pipeline only ever reads the file, so a file that shrinks
+  // mid-call gives SF_EIO, like the short read the reference would see.
+  const char* inpl = getenv("SF_FILE_INPLACE");
+  if (len && len >= inplace_min_bytes(true) && inpl && atoi(inpl)) {
     void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
     if (m != MAP_FAILED) {
       const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
@@ -1098,32 +1173,14 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
       munmap(m, len);
     }
   }
-  // Each stage is read by several threads in parallel (one pread stream per
-  // slice): one thread copies from the page cache at ~16 GB/s, below PCIe.
-  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
-  rc = index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
-    auto read_slice = [&](uint64_t a, uint64_t b) {
-      uint64_t got = a;
-      while (got < b) {
-        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(off + got));
-        if (r <= 0) return SF_EIO;
-        got += (uint64_t)r;
-      }
-      return SF_OK;
-    };
-    const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
-    std::vector<std::thread> pool;
-    std::vector<int> rcs(nthreads, SF_OK);
-    for (unsigned t = 1; t < nthreads && t * slice < n; t++)
-      pool.emplace_back([&, t] { rcs[t] = read_slice(t * slice, std::min(n, (t + 1) * slice)); });
-    rcs[0] = read_slice(0, std::min(n, slice));
-    for (auto& th : pool) th.join();
-    for (int r : rcs)
-      if (r) return r;
+  if (nb == 0) {
+    close(fd);
+    static const uint8_t none = 0;
+    if (blocks_hash) sf_host_sha1_impl(&none, 0, blocks_hash, 0);
     return SF_OK;
-  });
+  }
+  rc = index_file_pread(fd, len, block_size, out, blocks_hash);
   close(fd);
-  if (rc == SF_OK && blocks_hash) rc = sf_blocks_hash_sigs(out, nb, blocks_hash);
   return rc;
 }
 

@@ -186,11 +186,12 @@ def test_index_file_end_to_end(gpu):
     assert bh == oracle.blocks_hash(want)
 
 
-@pytest.mark.parametrize("no_mmap", ["0", "1"])
-def test_index_file_large_both_routes(gpu, no_mmap, monkeypatch):
-    # >= 16 MiB and in the page cache (just written): the mmap + hostRegister
-    # route; SF_NO_MMAP=1 forces the pread pipeline.  Same rows either way.
-    monkeypatch.setenv("SF_NO_MMAP", no_mmap)
+@pytest.mark.parametrize("inplace", ["0", "1"])
+def test_index_file_large_both_routes(gpu, inplace, monkeypatch):
+    # default: the pread pipeline; SF_FILE_INPLACE=1 (opt-in): >= 16 MiB and
+    # in the page cache (just written) -> the mmap + hostRegister route.
+    # Same rows either way.
+    monkeypatch.setenv("SF_FILE_INPLACE", inplace)
     data = oracle.splitmix_bytes((96 << 20) + 4093, 95)
     with tempfile.NamedTemporaryFile(delete=False) as f:
         f.write(data.tobytes())
@@ -268,12 +269,15 @@ def test_host_cache_reuse_release_and_threads(gpu, inplace_case):
     assert np.array_equal(got[0], want) and np.array_equal(got[1], want_small)
 
 
-@pytest.mark.parametrize("fail_at", ["", "1"])
-def test_index_file_inplace_multi_stage(gpu, inplace_case, fail_at, monkeypatch, tmp_path):
-    # a page-cache-resident file of 2.4 stages: mapped, locked region by
-    # region, blocks_hash folded in stage by stage
-    if fail_at:
-        monkeypatch.setenv("SF_INPLACE_FAIL_AT", fail_at)
+@pytest.mark.parametrize("route", ["pread", "inplace", "inplace_fail1"])
+def test_index_file_multi_stage(gpu, inplace_case, route, monkeypatch, tmp_path):
+    # a file of 2.4 stages, blocks_hash folded in stage by stage: the default
+    # pread pipeline; the opt-in in-place route (mapped, locked region by
+    # region); and the in-place route with regions >= 1 bounced via pread
+    if route != "pread":
+        monkeypatch.setenv("SF_FILE_INPLACE", "1")
+    if route == "inplace_fail1":
+        monkeypatch.setenv("SF_INPLACE_FAIL_AT", "1")
     data, want = inplace_case
     path = tmp_path / "f.bin"
     path.write_bytes(data[3:].tobytes())
@@ -390,3 +394,19 @@ def test_concurrent_host_threads_own_streams(gpu):
     for k in range(4):
         want = oracle.index_fixed(bufs[k], 4096)[2]
         assert np.array_equal(outs[k][0], want) and np.array_equal(outs[k][1], want)
+
+
+@pytest.mark.parametrize("n,bs,stage_mib", [((20 << 20) + 4095, 4096, "3"), ((7 << 20) + 1, 1000, "1"),
+                                           ((6 << 20), 65536, "1"), (4096 * 3, 4096, "1")])
+def test_index_file_pread_small_stages(gpu, monkeypatch, tmp_path, n, bs, stage_mib):
+    # the pread pipeline with small stages: many stage edges, rows and the
+    # streaming blocks_hash emitted stage by stage in file order
+    monkeypatch.setenv("SF_STREAM_STAGE_MIB", stage_mib)
+    data = oracle.splitmix_bytes(n, 990 + bs % 97)
+    path = tmp_path / "s.bin"
+    data.tofile(path)
+    rows, bh = host.index_file(str(path), bs)
+    offs, sizes, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(rows["sha1"], want)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    assert bh == oracle.blocks_hash(want)
