@@ -17,15 +17,16 @@ run() {  # name timeout cmd...
 if [ -n "$PROBE" ]; then
   run valu_probe 300 ./scripts/valu_probe || exit $?
 fi
-run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider
+run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 150 --timeout-method thread
 rc=$?; if [ $rc -ge 2 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 2 --cpu-seconds 8 || exit $?
 if [ -n "$EXTRA" ]; then
   run bench_c3 600 python bench.py --config 3 --steps "$STEPS" --warmup 2 --no-cpu-baseline || exit $?
   run bench_c5 600 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline || exit $?
-  # N>1 code path rehearsal on one GPU: 2 ranks share cuda:0, gloo gather
-  run bench_rehearsal2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --shard-gib 1 --dist-backend gloo || exit $?
+  # N>1 code path rehearsal on one GPU: bench.py starts its 2 ranks itself,
+  # both share cuda:0, gloo gather
+  run bench_rehearsal2 600 python bench.py --gpus 2 --steps 5 --warmup 1 --shard-gib 1 --dist-backend gloo --no-cpu-baseline || exit $?
 fi
 if [ -n "$PROFILE" ]; then
   B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
@@ -34,5 +35,7 @@ if [ -n "$PROFILE" ]; then
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o pmc -- $B || exit $?
   run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o pmc -- $B || exit $?
   python scripts/pmc_traffic.py gpurun_out/pmc_fetch/pmc_counter_collection.csv gpurun_out/pmc_write/pmc_counter_collection.csv config2 8589934592 gpurun_out/traffic.json
+  # the bench line again, now with this build's PMC traffic attached
+  run bench_traffic 600 python bench.py --steps "$STEPS" --warmup 2 --no-cpu-baseline --traffic-file gpurun_out/traffic.json || exit $?
 fi
 exit $rc

@@ -4,14 +4,18 @@ Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
 coalesced streaming read (16 B/lane loads and buffer_load ... lds alike), so it
 is doubled; WRITE_SIZE is exact for streaming stores.  Averages over every
-launch of the SHA-1 kernel in the pass.
+launch of the SHA-1 kernel in the pass.  The entry records the SHA-256 of the
+library the passes ran (bench.py reports traffic only for that same build).
 
 usage: python scripts/pmc_traffic.py FETCH_CSV WRITE_CSV CONFIG_KEY SHARD_BYTES [OUT]
 """
 import csv
+import hashlib
 import json
 import os
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "syncfast_amd", "lib", "libsyncfast_amd.so")
 
 
 def avg(path, counter, match="sha1_fixed_kernel"):
@@ -33,6 +37,7 @@ def main():
     data[key] = {"shard_bytes": shard, "hbm_bytes_per_launch": int(read_b + write_b),
                  "read_bytes": int(read_b), "write_bytes": int(write_b), "launches": [nf, nw],
                  "raw_kib": {"FETCH_SIZE": f, "WRITE_SIZE": w},
+                 "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
                  "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"}
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data[key]))
