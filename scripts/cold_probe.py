@@ -44,7 +44,11 @@ def main():
         path = f.name
     del data
     try:
+        # A/B interleaved: SF_FADVISE=1 (default: sequential + WILLNEED of the
+        # next stage) vs 0 (plain pread)
         for rep in range(2):
+          for adv in ("1", "0"):
+            os.environ["SF_FADVISE"] = adv
             fd = os.open(path, os.O_RDONLY)
             os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
             os.close(fd)
@@ -52,8 +56,8 @@ def main():
             t0 = time.perf_counter()
             rows, bh = host.index_file(path, 4096)
             t = time.perf_counter() - t0
-            print(f"sf_index_file {n / GiB:.0f} GiB cold (resident before: {fr:.3f}), incl. blocks_hash: "
-                  f"{n / t / 1e9:.2f} GB/s", flush=True)
+            print(f"sf_index_file {n / GiB:.0f} GiB cold (resident before: {fr:.3f}), SF_FADVISE={adv}, "
+                  f"incl. blocks_hash: {n / t / 1e9:.2f} GB/s", flush=True)
             t0 = time.perf_counter()
             host.index_file(path, 4096)
             t = time.perf_counter() - t0
