@@ -267,9 +267,13 @@ def main():
     # start+shard) of one logical file (seed SEED).
     data = torch.empty(shard, dtype=torch.uint8, device=dev)
     device.fill_splitmix(data, SEED, start)
-    # Two digest tables: step i writes table i%2 while the gather of step
-    # i-1's table is still in flight (RCCL runs on its own stream).
-    nbuf = 3 if (cfg["files"] > 1 and a.c3_mode == "stream") else 2  # split chains read batch i-2's table
+    # Rotating digest tables: step i writes table i%nbuf while the gathers of
+    # earlier steps' tables are still in flight (RCCL runs on its own stream).
+    # With a gather, three: RCCL's receive kernel on rank 0 may only get CUs
+    # once the next SHA-1 launch is fully dispatched, so the gather of step i
+    # can end during step i+1; with two tables step i+2 would wait for it.
+    gather = distributed and not a.no_gather
+    nbuf = 3 if (gather or (cfg["files"] > 1 and a.c3_mode == "stream")) else 2  # split chains read batch i-2's table
     digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     files = None
     if cfg["files"] > 1:
@@ -279,8 +283,7 @@ def main():
     status = torch.zeros(1, dtype=torch.int32, device=dev)  # staged batch: SF_ETIMEDOUT if a chain gave up
     if a.weak and files is not None:
         raise SystemExit("--weak applies to configs 2 and 5")
-    weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)] if a.weak else None
-    gather = distributed and not a.no_gather
+    weaks = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(nbuf)] if a.weak else None
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
