@@ -194,6 +194,17 @@ int sf_index_buffer(const uint8_t *data, uint64_t len, uint32_t block_size,
 int sf_index_file(const char *path, uint32_t block_size, sf_block_sig *out, uint64_t cap,
                   uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
 
+/* One shard of a file on disk: bytes [start, start+len) of a regular file
+ * (start a multiple of block_size; the shard's last block may be short only
+ * where the file ends), through the same pread pipeline as sf_index_file.
+ * Row offsets are FILE offsets, so the shards' rows concatenated in order
+ * are the file's rows (src/index.rs:629-656).  No blocks_hash: it chains
+ * over every digest of the file, so the rank that gathers the shards'
+ * digests computes it (sf_blocks_hash).  SF_ERANGE if the range passes the
+ * end of the file.  Blocking. */
+int sf_index_file_range(const char *path, uint64_t start, uint64_t len, uint32_t block_size,
+                        sf_block_sig *out, uint64_t cap, uint64_t *n_out);
+
 /* Sequential input from an open file descriptor (pipe, FIFO, socket, or a
  * file read from its current position), read to EOF: the rows of its fixed
  * tiling, offsets from the first byte read, in a buffer the library

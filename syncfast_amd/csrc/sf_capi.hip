@@ -1066,18 +1066,22 @@ inline bool fadvise_on() {
   return !e || atoi(e) != 0;
 }
 
-static int index_file_pread(int fd, uint64_t len, uint32_t bs, sf_block_sig* out, uint8_t* blocks_hash) {
+// Bytes [base, base + len) of the file (base a multiple of bs: a shard of
+// one logical file); row offsets are file offsets.
+static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf_block_sig* out,
+                            uint8_t* blocks_hash) {
   const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
   const bool adv = fadvise_on();
-  if (adv) (void)posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  if (adv) (void)posix_fadvise(fd, (off_t)base, (off_t)len, POSIX_FADV_SEQUENTIAL);
   auto fill = [&](uint8_t* dst, uint64_t off, uint64_t cap, uint64_t* nout, bool* eof) {
     const uint64_t n = std::min(cap, len - off);
     *nout = n;
     *eof = off + n >= len;
-    if (adv && !*eof) (void)posix_fadvise(fd, (off_t)(off + n), (off_t)std::min(cap, len - off - n), POSIX_FADV_WILLNEED);
+    if (adv && !*eof)
+      (void)posix_fadvise(fd, (off_t)(base + off + n), (off_t)std::min(cap, len - off - n), POSIX_FADV_WILLNEED);
     auto read_slice = [&](uint64_t a, uint64_t b) {
       for (uint64_t got = a; got < b;) {
-        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(off + got));
+        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(base + off + got));
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) return SF_EIO;
         got += (uint64_t)r;
@@ -1096,7 +1100,7 @@ static int index_file_pread(int fd, uint64_t len, uint32_t bs, sf_block_sig* out
     return SF_OK;
   };
   auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
-    write_rows(out + first, first, nb, dg, bytes, bs);
+    write_rows(out + first, base / bs + first, nb, dg, bytes, bs);
     return SF_OK;
   };
   return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
@@ -1191,7 +1195,26 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
     if (blocks_hash) sf_host_sha1_impl(&none, 0, blocks_hash, 0);
     return SF_OK;
   }
-  rc = index_file_pread(fd, len, block_size, out, blocks_hash);
+  rc = index_file_pread(fd, 0, len, block_size, out, blocks_hash);
+  close(fd);
+  return rc;
+}
+
+int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t block_size, sf_block_sig* out,
+                        uint64_t cap, uint64_t* n_out) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (!path || start % block_size) return SF_EINVAL;
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_out) *n_out = nb;
+  if (nb > cap) return SF_ENOSPC;
+  if (nb && !out) return SF_EINVAL;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return SF_EIO;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return SF_EIO; }
+  if (start > (uint64_t)sb.st_size || len > (uint64_t)sb.st_size - start) { close(fd); return SF_ERANGE; }
+  rc = nb ? index_file_pread(fd, start, len, block_size, out, nullptr) : SF_OK;
   close(fd);
   return rc;
 }

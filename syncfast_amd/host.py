@@ -63,6 +63,18 @@ def index_file(path, block_size: int) -> Tuple[np.ndarray, bytes]:
     return out[:nout.value], bytes(bh)
 
 
+def index_file_range(path, start: int, length: int, block_size: int) -> np.ndarray:
+    """Rows of bytes [start, start+length) of a file (one shard of it; start a
+    multiple of block_size), offsets relative to the file (sf_index_file_range)."""
+    n = (length + block_size - 1) // block_size if length else 0
+    out = np.zeros(max(n, 1), SIG_DTYPE)
+    nout = ctypes.c_uint64(0)
+    check(lib().sf_index_file_range(os.fsencode(path), start, length, block_size,
+                                    out.ctypes.data_as(ctypes.POINTER(BlockSig)), n, ctypes.byref(nout)),
+          "sf_index_file_range")
+    return out[:nout.value]
+
+
 def index_fd(fd: int, block_size: int) -> Tuple[np.ndarray, bytes]:
     """Signatures of everything readable from an open descriptor (a pipe, a
     FIFO, ...) to EOF + its blocks_hash (sf_index_fd: sequential route, rows

@@ -80,3 +80,42 @@ def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
     if async_op:
         return work, finish
     return finish()
+
+
+def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup] = None, dst: int = 0,
+                       device: Optional[torch.device] = None):
+    """One file on disk indexed by every rank of the group, each on its own
+    GPU: rank r reads and hashes its shard_range of the file
+    (sf_index_file_range, pread pipeline on the rank's current device), the
+    shards' digest tables are gathered to `dst`, which rebuilds the file's rows
+    and computes its blocks_hash (src/index.rs:661-682 chains over every
+    digest, so it runs once, after the gather).
+
+    Returns (rows SIG_DTYPE[n], blocks_hash bytes) on `dst`, None elsewhere.
+    `device`: where the gather's tensors live (the rank's GPU for RCCL; None
+    = host tensors, for gloo)."""
+    import os
+
+    import numpy as np
+
+    from . import host
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    size = os.path.getsize(path)
+    start, ln = shard_range(size, block_size, world, rank)
+    rows = host.index_file_range(path, start, ln, block_size)
+    dig = torch.from_numpy(np.ascontiguousarray(rows["sha1"]).reshape(-1, 20))
+    if device is not None:
+        dig = dig.to(device)
+    table = gather_digests(dig, size, block_size, group=group, dst=dst)
+    if rank != dst:
+        return None
+    table = table.cpu().numpy()
+    n = table.shape[0]
+    out = np.zeros(n, host.SIG_DTYPE)
+    out["offset"] = np.arange(n, dtype=np.uint64) * block_size
+    out["size"] = block_size
+    if n:
+        out["size"][-1] = size - (n - 1) * block_size
+    out["sha1"] = table
+    return out, host.blocks_hash(table)

@@ -86,3 +86,71 @@ def test_bench_self_launches_two_ranks(gpu):
     assert line["n_gpus"] == 2 and line["config"]["total_bytes"] == 2 * (64 << 20)
     assert line["config"]["parallelism"].startswith("shard2+gloo_gather")
     assert line["value"] > 0
+
+
+def test_index_file_range_shards_concatenate(gpu, tmp_path):
+    # sf_index_file_range: every shard_range piece of a file on disk, rows
+    # with FILE offsets; concatenated in rank order = sf_index_file's rows
+    from syncfast_amd import host
+    from syncfast_amd._lib import SF_EINVAL, SF_ERANGE, SfError
+    from syncfast_amd.shard import shard_range
+    bs = 4096
+    data = oracle.splitmix_bytes((40 << 20) + 777, 0x5EED0005)
+    p = tmp_path / "f.bin"
+    data.tofile(p)
+    whole, bh = host.index_file(p, bs)
+    for world in (1, 2, 3, 8):
+        parts = [host.index_file_range(p, *shard_range(data.size, bs, world, r), bs) for r in range(world)]
+        assert np.concatenate(parts).tobytes() == whole.tobytes(), world
+    assert host.index_file_range(p, data.size, 0, bs).size == 0
+    with pytest.raises(SfError) as e:
+        host.index_file_range(p, 100, 4096, bs)  # start not block-aligned
+    assert e.value.code == SF_EINVAL
+    with pytest.raises(SfError) as e:
+        host.index_file_range(p, 4096, data.size, bs)  # past the end
+    assert e.value.code == SF_ERANGE
+
+
+def _file_rank(rank, world, port, path, bs, q):
+    import torch.distributed as dist
+
+    from syncfast_amd.shard import index_file_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = index_file_sharded(path, bs)
+        if rank == 0:
+            rows, bh = res
+            q.put((rows.tobytes(), bh))
+        else:
+            assert res is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_index_file_sharded_two_ranks(gpu, tmp_path):
+    # one file on disk, two ranks (sharing the box's GPU, gloo gather): rank 0
+    # holds the whole file's rows and blocks_hash, equal to the oracle's
+    import torch.multiprocessing as mp
+
+    from syncfast_amd import host
+    bs = 65536
+    data = oracle.splitmix_bytes((24 << 20) + 12345, 0x5EED0006)
+    p = tmp_path / "g.bin"
+    data.tofile(p)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_file_rank, args=(r, 2, port, str(p), bs, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    rows_b, bh = q.get(timeout=100)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    rows = np.frombuffer(rows_b, host.SIG_DTYPE)
+    offs, sizes, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    assert np.array_equal(np.stack([r["sha1"] for r in rows]), want)
+    assert bh == oracle.blocks_hash(want)

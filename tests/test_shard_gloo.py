@@ -73,3 +73,55 @@ def test_gather_matches_whole_file(world, total, bs):
     _, _, want = oracle.index_fixed(whole, bs)
     assert got == want.tobytes() and got_async == want.tobytes()
     assert oracle.blocks_hash(np.frombuffer(got, np.uint8)) == oracle.blocks_hash(want)
+
+
+def _fake_index_file_range(path, start, length, bs):
+    """CPU stand-in for sf_index_file_range (no GPU here): the oracle's rows of
+    the byte range, file offsets -- only the shard/gather/rebuild logic of
+    index_file_sharded is under test."""
+    from syncfast_amd.host import SIG_DTYPE
+    data = np.fromfile(path, np.uint8)[start:start + length]
+    offs, sizes, dig = oracle.index_fixed(data, bs)
+    out = np.zeros(offs.size, SIG_DTYPE)
+    out["offset"], out["size"], out["sha1"] = offs + start, sizes, dig
+    return out
+
+
+def _file_worker(rank, world, port, path, bs, q):
+    import syncfast_amd.host as h
+    from syncfast_amd.shard import index_file_sharded
+    h.index_file_range = _fake_index_file_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = index_file_sharded(path, bs)
+        if rank == 0:
+            q.put((res[0].tobytes(), res[1]))
+        else:
+            assert res is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total,bs", [(2, 4096 * 37 + 100, 4096), (3, 65536 * 5 + 1, 65536), (3, 10, 4096)])
+def test_index_file_sharded_rebuilds_rows(tmp_path, world, total, bs):
+    from syncfast_amd.host import SIG_DTYPE
+    p = tmp_path / "f"
+    data = oracle.splitmix_bytes(total, 0x5EED0007)
+    data.tofile(p)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_file_worker, args=(r, world, port, str(p), bs, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    rows_b, bh = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    rows = np.frombuffer(rows_b, SIG_DTYPE)
+    offs, sizes, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    assert np.array_equal(rows["sha1"], want)
+    assert bh == oracle.blocks_hash(want)
