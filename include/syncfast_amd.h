@@ -195,8 +195,9 @@ int sf_index_file(const char *path, uint32_t block_size, sf_block_sig *out, uint
                   uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
 
 /* One shard of a file on disk: bytes [start, start+len) of a regular file
- * (start a multiple of block_size; the shard's last block may be short only
- * where the file ends), through the same pread pipeline as sf_index_file.
+ * (start a multiple of block_size unless len == 0; the shard's last block
+ * may be short only where the file ends), through the same pread pipeline
+ * as sf_index_file.
  * Row offsets are FILE offsets, so the shards' rows concatenated in order
  * are the file's rows (src/index.rs:629-656).  No blocks_hash: it chains
  * over every digest of the file, so the rank that gathers the shards'

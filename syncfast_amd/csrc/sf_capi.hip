@@ -1204,7 +1204,7 @@ int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t
                         uint64_t cap, uint64_t* n_out) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
-  if (!path || start % block_size) return SF_EINVAL;
+  if (!path || (len && start % block_size)) return SF_EINVAL;  // an empty shard may start anywhere up to EOF
   const uint64_t nb = len ? ceil_div(len, block_size) : 0;
   if (n_out) *n_out = nb;
   if (nb > cap) return SF_ENOSPC;

@@ -102,7 +102,11 @@ def test_index_file_range_shards_concatenate(gpu, tmp_path):
     for world in (1, 2, 3, 8):
         parts = [host.index_file_range(p, *shard_range(data.size, bs, world, r), bs) for r in range(world)]
         assert np.concatenate(parts).tobytes() == whole.tobytes(), world
-    assert host.index_file_range(p, data.size, 0, bs).size == 0
+    assert host.index_file_range(p, data.size, 0, bs).size == 0  # an empty shard at EOF (unaligned start)
+    small = tmp_path / "small.bin"
+    data[:10].tofile(small)
+    pieces = [host.index_file_range(small, *shard_range(10, bs, 3, r), bs) for r in range(3)]
+    assert [x.size for x in pieces] == [1, 0, 0]
     with pytest.raises(SfError) as e:
         host.index_file_range(p, 100, 4096, bs)  # start not block-aligned
     assert e.value.code == SF_EINVAL
