@@ -269,9 +269,9 @@ def main():
     device.fill_splitmix(data, SEED, start)
     # Rotating digest tables: step i writes table i%nbuf while the gathers of
     # earlier steps' tables are still in flight (RCCL runs on its own stream).
-    # With a gather, three: RCCL's receive kernel on rank 0 may only get CUs
-    # once the next SHA-1 launch is fully dispatched, so the gather of step i
-    # can end during step i+1; with two tables step i+2 would wait for it.
+    # With a gather, three, so a gather may run into step i+2 without stalling
+    # it (simulated on one GPU, scripts/gather_sim.py: 2, 3 and 4 tables all
+    # cost rank 0 the same +3.7 %, the receive traffic itself).
     gather = distributed and not a.no_gather
     nbuf = 3 if (gather or (cfg["files"] > 1 and a.c3_mode == "stream")) else 2  # split chains read batch i-2's table
     digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=dev) for _ in range(nbuf)]

@@ -56,9 +56,11 @@ def main():
         device.index_device(data, 4096)
     torch.cuda.synchronize()
     res = {}
-    for rep in range(3):
-        for name, nbuf, side in (("no gather", 2, False), ("nbuf=2", 2, True), ("nbuf=3", 3, True)):
-            ms = run(data, nbuf, 20, recv, side)
+    reps, steps = int(os.environ.get("SIM_REPS", "6")), int(os.environ.get("SIM_STEPS", "40"))
+    for rep in range(reps):
+        for name, nbuf, side in (("no gather", 2, False), ("nbuf=2", 2, True), ("nbuf=3", 3, True),
+                                 ("nbuf=4", 4, True)):
+            ms = run(data, nbuf, steps, recv, side)
             res.setdefault(name, []).append(ms)
             print(f"rep {rep} {name}: {ms:.3f} ms/step", flush=True)
     for k, v in res.items():
