@@ -21,7 +21,8 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
                    time (HIP events on the launch stream) vs 8.0 TB/s HBM peak;
                    traffic = HBM bytes per launch from rocprofv3 PMC counters
                    (profiles/traffic.json, measured separately on the SAME
-                   library build -- keyed by the .so's SHA-256 -- else null);
+                   kernels -- keyed by the SHA-256 of the library's gfx950
+                   code objects -- else null);
   cpu_baseline  -- the C oracle (single-threaded SHA-1 port of the
                    reference loop) on a bounded sample of the same bytes, rank 0
                    at N=1 only; cpu_baseline_shani the same tiling with the
@@ -132,7 +133,7 @@ def check_launch(a, world, rank) -> None:
 
 
 def lib_sha256() -> str:
-    """SHA-256 of the HIP library this process runs (keys profiles/traffic.json)."""
+    """SHA-256 of the HIP library this process runs."""
     from syncfast_amd._lib import LIB_PATH
     h = hashlib.sha256()
     with open(LIB_PATH, "rb") as f:
@@ -406,16 +407,18 @@ def main():
     if weaks is not None:  # + 4 B weak sum written per block
         alg_bytes += nblk * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    # PMC traffic of the same kernel on the same library build (else null:
-    # numbers from another build are stale).
+    # PMC traffic of the same kernels (same gfx950 code objects; else null:
+    # numbers from other kernels are stale).
+    from syncfast_amd._lib import code_object_sha256
     traffic = None
     build = lib_sha256()
+    kernels = code_object_sha256()
     try:
         with open(a.traffic_file) as f:
             tr = json.load(f)
         key = f"config{a.config}"
         ent = tr.get(key, {})
-        if ent.get("shard_bytes") == shard and ent.get("lib_sha256") == build and not a.weak:
+        if ent.get("shard_bytes") == shard and ent.get("code_object_sha256") == kernels and not a.weak:
             traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
@@ -465,6 +468,7 @@ def main():
         "cpu_baseline_shani_all_cores": cpu_ni_all,
         "config1": config1_probe() if world == 1 else None,
         "lib_sha256": build,
+        "code_object_sha256": kernels,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
     }

@@ -125,6 +125,28 @@ def check(rc: int, what: str = "") -> None:
         raise SfError(rc, what)
 
 
+def code_object_sha256(path: str = None) -> str:
+    """SHA-256 of the gfx950 code objects inside the library (its
+    ``.hip_fatbin`` section): what the GPU runs.  Host-only changes to the
+    library leave it unchanged; any kernel change alters it.  bench.py keys
+    the PMC traffic of profiles/traffic.json on it."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as f:
+        b = f.read()
+    if b[:4] != b"\x7fELF" or b[4] != 2:
+        raise ValueError("not an ELF64 library")
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stro = secs[shstrndx][4]
+    for sec in secs:
+        name = b[stro + sec[0]: b.index(b"\0", stro + sec[0])]
+        if name == b".hip_fatbin":
+            return hashlib.sha256(b[sec[4]: sec[4] + sec[5]]).hexdigest()
+    raise ValueError("no .hip_fatbin section")
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     check(lib().sf_device_count(ctypes.byref(n)), "sf_device_count")

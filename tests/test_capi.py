@@ -162,3 +162,17 @@ def test_product_does_not_import_oracle():
                 src = open(os.path.join(dirpath, fn), errors="replace").read()
                 assert "import oracle" not in src and "from oracle" not in src, fn
                 assert "sf_oracle" not in src and "sfo_" not in src, fn
+
+
+def test_traffic_profile_is_for_these_kernels():
+    # bench.py reports roofline.traffic only when profiles/traffic.json was
+    # measured on the same gfx950 code objects; this keeps the committed PMC
+    # pass in step with the kernels (refresh it after any kernel change:
+    # PROFILE=1 scripts/gpu_round.sh, then scripts/pmc_traffic.py)
+    import json
+    from syncfast_amd._lib import code_object_sha256
+    h = code_object_sha256()
+    assert len(h) == 64
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tr = json.load(f)
+    assert tr["config2"]["code_object_sha256"] == h
