@@ -97,3 +97,20 @@ def test_index_files_large_mapped_and_pread(gpu, tmp_path, stage, no_mmap, monke
     paths = _write(tmp_path, eq, 2200)
     rows, first, fh = host.index_files(paths, 4096, stage_bytes=stage)
     _check(paths, eq, 2200, 4096, rows, first, fh)
+
+
+@pytest.mark.gpu
+def test_index_files_reports_the_failing_file(gpu, tmp_path):
+    # a missing file and a directory in the list: SF_EIO naming the first
+    # failing file (the error the per-file loop would raise at File::open)
+    from syncfast_amd._lib import SfError
+    paths = _write(tmp_path, [100, 5000, 7], 3100)
+    missing = tmp_path / "gone"
+    with pytest.raises(SfError) as e:
+        host.index_files(paths[:2] + [missing] + paths[2:], 4096)
+    assert e.value.code == -5 and str(missing) in str(e.value)
+    with pytest.raises(SfError) as e:
+        host.index_files([paths[0], tmp_path, paths[1]], 4096)
+    assert e.value.code == -5 and str(tmp_path) in str(e.value)
+    rows, first, fh = host.index_files(paths, 4096)  # and the call after an error is clean
+    _check(paths, [100, 5000, 7], 3100, 4096, rows, first, fh)

@@ -243,3 +243,29 @@ def test_walk_visits_entries_in_readdir_order(tmp_path):
 
     assert [str(r) for _p, r in todo] == [str(r) for r in expect(PurePath(""))]
     assert len(todo) == 12
+
+
+@pytest.mark.gpu
+def test_mtime_gate_at_nanosecond_resolution(gpu, tmp_path):
+    # src/index.rs:183 compares DateTime values: a file whose mtime moved by
+    # 1 us is re-indexed; one rewritten with its exact old mtime is not (the
+    # reference's gate cannot see that either)
+    root = tmp_path / "t"
+    root.mkdir()
+    p = root / "f"
+    p.write_bytes(oracle.splitmix_bytes(50_000, 1).tobytes())
+    t0 = 1_700_000_000_123_456_789
+    os.utime(p, ns=(t0, t0))
+    idx = Index.open_in_memory(chunker=FixedChunker(4096))
+    idx.index_path(root)
+    fid, m, bh1 = idx.get_file("f")
+    assert m.ns == os.stat(p).st_mtime_ns
+    p.write_bytes(oracle.splitmix_bytes(50_000, 2).tobytes())
+    os.utime(p, ns=(t0, m.ns))  # same stored instant
+    idx.index_path(root)
+    assert idx.get_file("f")[2] == bh1  # gate: up to date
+    os.utime(p, ns=(t0, m.ns + 1000))
+    idx.index_path(root)
+    bh2 = idx.get_file("f")[2]
+    want = oracle.index_fixed(oracle.splitmix_bytes(50_000, 2), 4096)[2]
+    assert bh2.bytes == oracle.blocks_hash(want) != bh1.bytes
