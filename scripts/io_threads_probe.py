@@ -1,4 +1,4 @@
-"""sf_index_files over 0-200 KiB files and 8 MiB files with 4/8/16 reader
+"""sf_index_files over 0-200 KiB files and 8 MiB files with 8/12/16/24 reader
 threads (SF_IO_THREADS), files in the page cache."""
 import os
 import sys
@@ -30,7 +30,7 @@ with tempfile.TemporaryDirectory(dir=os.environ.get("E2E_DIR", "/tmp")) as td:
         big.append(p)
     for name, paths, nbytes in (("0-200 KiB", small, off), ("8 MiB", big, 1 << 30)):
         host.index_files(paths, 4096)
-        for th in ("4", "8", "16", "8", "16"):
+        for th in ("8", "12", "16", "24", "8", "12", "16", "24"):
             os.environ["SF_IO_THREADS"] = th
             t0 = time.perf_counter()
             host.index_files(paths, 4096)
