@@ -1266,6 +1266,9 @@ struct StageMaps {
 };
 
 // Files of a stage that are DMA'd from their page-locked mappings instead of
+// being read (opt-in; like SF_FILE_INPLACE, a file truncated while its
+// registered mapping is being copied hangs the queues, so it is off unless
+// asked for).
 // being read into the pinned stage: none by default.  With the per-device
 // cache, the 8-thread pread stage beats per-file registration at every size
 // measured (scripts/map_min_probe.py: 16 MiB files 40 vs 23 GB/s, 64 MiB 46
