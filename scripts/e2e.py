@@ -82,11 +82,15 @@ def wire_rate():
     torch.cuda.synchronize()
     with open("/dev/null", "wb") as f:
         wire.file_blocks_to_fd(dig, 4096, n, f.fileno())  # warm up
-        t0 = time.perf_counter()
-        nbytes = wire.file_blocks_to_fd(dig, 4096, n, f.fileno())
-        dt = time.perf_counter() - t0
-    print(f"wire: FILE_BLOCK run of 2^21 blocks ({nbytes / 1e6:.1f} MB) to an fd: {nbytes / dt / 1e9:.2f} GB/s "
-          f"({dig.shape[0] / dt / 1e6:.1f} M messages/s)", flush=True)
+        for rep in range(2):
+            for chunk in ("65536", "262144", "1048576"):  # messages per chunk (SF_WIRE_CHUNK; default 262144)
+                os.environ["SF_WIRE_CHUNK"] = chunk
+                t0 = time.perf_counter()
+                nbytes = wire.file_blocks_to_fd(dig, 4096, n, f.fileno())
+                dt = time.perf_counter() - t0
+                print(f"wire: FILE_BLOCK run of 2^21 blocks ({nbytes / 1e6:.1f} MB) to an fd, chunk {chunk}: "
+                      f"{nbytes / dt / 1e9:.2f} GB/s ({dig.shape[0] / dt / 1e6:.1f} M messages/s)", flush=True)
+        del os.environ["SF_WIRE_CHUNK"]
 
 
 def many_files(data, d):
@@ -137,4 +141,7 @@ def many_files(data, d):
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("E2E_ONLY") == "wire":
+        wire_rate()
+    else:
+        main()

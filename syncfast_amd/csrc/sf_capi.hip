@@ -221,21 +221,10 @@ int check_fixed_args(uint64_t len, uint32_t bs) {
   return SF_OK;
 }
 
-// RAII device / pinned allocations for the host-memory entry points.
-struct DevBuf {
-  void* p = nullptr;
-  ~DevBuf() { if (p) (void)hipFree(p); }
-};
+// RAII pinned allocation (the in-place route's bounce buffer).
 struct PinBuf {
   void* p = nullptr;
   ~PinBuf() { if (p) (void)hipHostFree(p); }
-};
-struct Streams {
-  hipStream_t s[2] = {nullptr, nullptr};
-  ~Streams() {
-    for (auto x : s)
-      if (x) (void)hipStreamDestroy(x);
-  }
 };
 
 // Per-device resources of the host-memory entry points (streams, events,
@@ -675,6 +664,11 @@ int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_
   return hip_err(hipGetLastError());
 }
 
+#ifndef SF_WIRE_CHUNK_DEFAULT
+#define SF_WIRE_CHUNK_DEFAULT (1ull << 18)
+#endif
+static constexpr uint64_t kWireChunk = SF_WIRE_CHUNK_DEFAULT;  // messages per chunk (~9.4 MB at 4 KiB blocks)
+
 int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
                            uint64_t* n_written, void* stream) {
   if (n_written) *n_written = 0;
@@ -690,28 +684,32 @@ int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t bl
   for (uint64_t v = last; v >= 10; v /= 10) dl++;
   const uint64_t msg = 33 + db;  // every message but the last
   const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
-  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : (1ull << 20));
+  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : kWireChunk);
   const uint64_t nchunks = ceil_div(nb, per);
   const uint64_t cap = std::min(per, nb) * msg + (33 + dl);
-  Streams st;
-  DevBuf dout[2];
-  PinBuf pin[2];
-  hipEvent_t ev[2] = {nullptr, nullptr}, ready = nullptr;
+  // Streams, events and the two chunk buffers (device + pinned) come from the
+  // per-device set the other host entry points keep between calls: pinning
+  // two chunk buffers per call cost more than the call's copies.
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* ev;
+  void *dout[2], *pin[2];
+  hipEvent_t ready = nullptr;
   uint64_t bytes_of[2] = {0, 0};
-  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-  SF_HIP(hipEventRecord(ready, as_stream(stream)));  // the digests are produced on the caller's stream
-  for (int i = 0; i < 2; i++) {
-    SF_HIP(hipStreamCreateWithFlags(&st.s[i], hipStreamNonBlocking));
-    SF_HIP(hipStreamWaitEvent(st.s[i], ready, 0));
-    SF_HIP(hipMalloc(&dout[i].p, cap));
-    SF_HIP(hipHostMalloc(&pin[i].p, cap, hipHostMallocDefault));
-    SF_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  int rc = res.streams(st, ev);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, cap, &dout[i]);
+    if (rc == SF_OK) rc = res.pin(i, cap, &pin[i]);
   }
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  if (hipEventRecord(ready, as_stream(stream)) != hipSuccess ||  // the digests are produced on the caller's stream
+      hipStreamWaitEvent(st[0], ready, 0) != hipSuccess || hipStreamWaitEvent(st[1], ready, 0) != hipSuccess)
+    rc = SF_ENODEV;
   uint64_t written = 0;
-  int rc = SF_OK;
   auto flush = [&](int b) {  // write chunk buffer b to fd, in order
     if (hipEventSynchronize(ev[b]) != hipSuccess) return SF_ENODEV;
-    const uint8_t* p = static_cast<const uint8_t*>(pin[b].p);
+    const uint8_t* p = static_cast<const uint8_t*>(pin[b]);
     for (uint64_t done = 0; done < bytes_of[b];) {
       const ssize_t w = write(fd, p + done, bytes_of[b] - done);
       if (w < 0 && errno == EINTR) continue;
@@ -730,19 +728,16 @@ int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t bl
     const bool final_chunk = i0 + n == nb;
     const uint32_t lsz = final_chunk ? last : block_size;
     bytes_of[b] = (n - 1) * msg + (final_chunk ? 33 + dl : msg);
-    hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st.s[b],
+    hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st[b],
                        static_cast<const uint8_t*>(d_digests) + i0 * 20, n, block_size, lsz,
-                       static_cast<uint8_t*>(dout[b].p));
+                       static_cast<uint8_t*>(dout[b]));
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(pin[b].p, dout[b].p, bytes_of[b], hipMemcpyDeviceToHost, st.s[b]) != hipSuccess ||
-        hipEventRecord(ev[b], st.s[b]) != hipSuccess)
+        hipMemcpyAsync(pin[b], dout[b], bytes_of[b], hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(ev[b], st[b]) != hipSuccess)
       rc = SF_ENODEV;
   }
   for (uint64_t k = nchunks >= 2 ? nchunks - 2 : 0; k < nchunks && rc == SF_OK; k++) rc = flush((int)(k & 1));
-  for (int i = 0; i < 2; i++) {
-    (void)hipStreamSynchronize(st.s[i]);
-    (void)hipEventDestroy(ev[i]);
-  }
+  for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(st[i]);
   (void)hipEventDestroy(ready);
   if (n_written) *n_written = written;
   return rc;
