@@ -525,7 +525,7 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   if (n_blocks) *n_blocks = total;
   if (total > cap_blocks) return SF_ENOSPC;
   if (n_files == 0) return SF_OK;
-  if (!d_data || (total && !d_digests)) return SF_EINVAL;
+  if ((!d_data && len) || (total && !d_digests)) return SF_EINVAL;  // all-empty files need no data
 
   // Equal-size, block-aligned, back-to-back files: the block table is a fixed
   // tiling of the batch, and each file's digest run is a fixed tiling of the
