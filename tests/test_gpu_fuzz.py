@@ -46,7 +46,7 @@ def _dev(data, gpu, shift):
     return t[shift:]
 
 
-@pytest.mark.parametrize("case", range(40))
+@pytest.mark.parametrize("case", range(160))
 def test_fuzz_fixed_device(gpu, case):
     rng = np.random.default_rng(10_000 + case)
     bs = _bs(rng)
@@ -58,7 +58,7 @@ def test_fuzz_fixed_device(gpu, case):
     assert got.shape == want.shape and np.array_equal(got, want), (n, bs)
 
 
-@pytest.mark.parametrize("case", range(25))
+@pytest.mark.parametrize("case", range(100))
 def test_fuzz_explicit_blocks(gpu, case):
     rng = np.random.default_rng(11_000 + case)
     n = int(rng.integers(0, 2 << 20))
@@ -73,7 +73,7 @@ def test_fuzz_explicit_blocks(gpu, case):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes)), (n, m)
 
 
-@pytest.mark.parametrize("case", range(25))
+@pytest.mark.parametrize("case", range(100))
 def test_fuzz_batch(gpu, case):
     # many files in one buffer: equal and ragged mixes, zero-length files,
     # files at 16-B aligned and unaligned offsets
@@ -100,7 +100,7 @@ def test_fuzz_batch(gpu, case):
         assert bytes(fh[k]) == oracle.blocks_hash(want), (k, ln, bs)
 
 
-@pytest.mark.parametrize("case", range(15))
+@pytest.mark.parametrize("case", range(60))
 def test_fuzz_host_routes(gpu, case, tmp_path, monkeypatch):
     # one input through the buffer, file, fd and file-range entry points,
     # with small pipeline stages so stage edges land anywhere
@@ -137,7 +137,7 @@ def test_fuzz_host_routes(gpu, case, tmp_path, monkeypatch):
     same(np.concatenate(parts))
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(30))
 def test_fuzz_index_files(gpu, case, tmp_path):
     rng = np.random.default_rng(14_000 + case)
     bs = _bs(rng)
