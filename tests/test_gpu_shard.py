@@ -158,3 +158,42 @@ def test_index_file_sharded_two_ranks(gpu, tmp_path):
     assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
     assert np.array_equal(np.stack([r["sha1"] for r in rows]), want)
     assert bh == oracle.blocks_hash(want)
+
+
+def _rccl_world1(port, q):
+    import torch
+    import torch.distributed as dist
+
+    from syncfast_amd import device
+    from syncfast_amd.shard import gather_digests
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        n, bs = (16 << 20) + 5, 4096
+        data = device.splitmix_tensor(n, 0x5EED0008, dev)
+        dig = device.index_device(data, bs)
+        full = gather_digests(dig, n, bs)  # RCCL gather (to itself), synchronous form
+        work, finish = gather_digests(dig, n, bs, async_op=True)
+        work.wait()
+        full2 = finish()
+        torch.cuda.synchronize()
+        ok = full.device.type == "cuda" and torch.equal(full, dig) and torch.equal(full2, dig)
+        q.put((ok, dig.cpu().numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_gather_path_world1(gpu):
+    # the bench's RCCL code path (backend "nccl" = RCCL on ROCm, device
+    # tensors, sync and async gathers) on the one GPU of this box
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1, args=(_free_port(), q))
+    p.start()
+    ok, got = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok
+    n, bs = (16 << 20) + 5, 4096
+    assert got == oracle.index_fixed(oracle.splitmix_bytes(n, 0x5EED0008), bs)[2].tobytes()
