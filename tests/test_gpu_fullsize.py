@@ -138,3 +138,25 @@ def test_config3_1024x8mib_every_digest_and_blocks_hash(gpu, mode):
     per_file = want.reshape(nf, -1, 20)
     wrong = [f for f in range(nf) if bytes(fh[f]) != host.blocks_hash(per_file[f])]
     assert not wrong, f"{len(wrong)} blocks_hash differ, first files {wrong[:5]}"
+
+
+def test_config4_whole_256gib_file_on_one_gpu(gpu):
+    # configs[3]'s whole logical file (256 GiB, 4 KiB blocks, 2^26 digests)
+    # fits in one MI355X's 288 GB: indexed whole and as its 8 shard_range
+    # shards (the 8-GPU layout) -- the concatenated shard tables equal the
+    # whole launch -- and every digest checked against the oracle, streamed
+    # back in 8 GiB pieces.  Skipped on a device with less free memory.
+    from syncfast_amd.shard import shard_range
+    n, bs = 256 * GiB, 4096
+    free, _ = torch.cuda.mem_get_info(gpu)
+    if free < n + (3 << 30):
+        pytest.skip(f"needs {n + (3 << 30)} B of free device memory, {free} free")
+    data = device.splitmix_tensor(n, 0x5EED0003, gpu)
+    whole = device.index_device(data, bs)
+    parts = torch.empty_like(whole)
+    for r in range(8):
+        s, ln = shard_range(n, bs, 8, r)
+        device.index_device(data[s:s + ln], bs, out=parts[s // bs:(s + ln) // bs])
+    assert torch.equal(parts, whole)
+    del parts
+    _check_streamed(data, whole.cpu().numpy(), bs, piece=8 * GiB)
