@@ -1,0 +1,74 @@
+"""The C-ABI from plain C (examples/sf_index.c): no Python, no PyTorch in the
+process -- what a Rust extern "C" binding amounts to.
+
+CPU: the binary builds, links only libsyncfast_amd (+ the HIP runtime) and
+fails loudly without a device.  GPU: a regular file, a FIFO and stdin give
+the oracle's rows and blocks_hash (src/index.rs:621-682)."""
+import os
+import subprocess
+import threading
+
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "examples", "build", "sf_index")
+
+
+def _built():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "examples")])
+    return BIN
+
+
+def _parse(out):
+    files, cur = {}, None
+    for ln in out.splitlines():
+        f = ln.split()
+        if f[0] == "file":
+            cur = files.setdefault(f[1], {"rows": []})
+        elif f[0] == "blocks_hash":
+            cur["bh"] = f[1]
+        else:
+            cur["rows"].append((int(f[0]), int(f[1]), f[2]))
+    return files
+
+
+def _want(data, bs):
+    offs, sizes, dig = oracle.index_fixed(data, bs)
+    return [(int(o), int(s), bytes(d).hex()) for o, s, d in zip(offs, sizes, dig)], oracle.blocks_hash(dig).hex()
+
+
+def test_c_consumer_fails_loudly_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    r = subprocess.run([_built(), "/dev/null"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_c_consumer_file_fifo_stdin(gpu, tmp_path):
+    exe = _built()
+    bs = 4096
+    a = oracle.splitmix_bytes((3 << 20) + 77, 31)
+    b = oracle.splitmix_bytes(10_000, 32)
+    pa, fifo = tmp_path / "a.bin", tmp_path / "pipe"
+    a.tofile(pa)
+    os.mkfifo(fifo)
+
+    def feed():
+        with open(fifo, "wb") as w:
+            w.write(b.tobytes())
+    th = threading.Thread(target=feed)
+    th.start()
+    r = subprocess.run([exe, "-b", str(bs), str(pa), str(fifo), "-"], input=a[:5000].tobytes(),
+                       capture_output=True, timeout=120)
+    th.join(timeout=30)
+    assert r.returncode == 0, r.stderr.decode()
+    got = _parse(r.stdout.decode())
+    for name, data in ((str(pa), a), (str(fifo), b), ("-", a[:5000])):
+        rows, bh = _want(data, bs)
+        assert got[name]["rows"] == rows and got[name]["bh"] == bh, name
+    r = subprocess.run([exe, str(tmp_path / "missing")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "I/O error" in r.stderr
