@@ -16,8 +16,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "examples", "build", "sf_index")
 
 
-def _built():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "examples")])
+def _built(make: bool):
+    """The example binary; built here on the CPU side (make is a no-op when it
+    is up to date), only looked up on a GPU box (built by build())."""
+    if make:
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "examples")])
+    assert os.path.exists(BIN), f"{BIN} not built: run __graft_entry__.build()"
     return BIN
 
 
@@ -43,13 +47,13 @@ def test_c_consumer_fails_loudly_without_device():
     import torch
     if torch.cuda.is_available():
         pytest.skip("a device is present")
-    r = subprocess.run([_built(), "/dev/null"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([_built(True), "/dev/null"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "no HIP device" in r.stderr
 
 
 @pytest.mark.gpu
 def test_c_consumer_file_fifo_stdin(gpu, tmp_path):
-    exe = _built()
+    exe = _built(False)
     bs = 4096
     a = oracle.splitmix_bytes((3 << 20) + 77, 31)
     b = oracle.splitmix_bytes(10_000, 32)
