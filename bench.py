@@ -27,6 +27,9 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
                    reference loop) on a bounded sample of the same bytes, rank 0
                    at N=1 only; cpu_baseline_shani the same tiling with the
                    product's SHA-NI host SHA-1, on 1 core and on all cores;
+  e2e_host_buffer -- not `value`: the same bytes from a host buffer through
+                   sf_index_buffer (H2D + kernel + D2H rows), beside the raw
+                   pinned H2D rate (north_star asks for the end-to-end rate);
   config1       -- BASELINE configs[0] (the unmodified Rust CPU path): probed
                    live (cargo / rustc on this host) and reported as not
                    runnable when they are absent.
@@ -90,6 +93,8 @@ def parse():
                    help="setup: keep the kernel busy this long before the warmup steps (the chip takes "
                         "~6 launches to ramp its clock from ~1.6 GHz; see DESIGN.md section 4)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the end-to-end leg (the same bytes from a host buffer through sf_index_buffer)")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--c3-mode", default="stream", choices=("stream", "staged"),
                    help="config 3: 'stream' = batch after batch, each launch also finishing the previous batch's "
@@ -176,6 +181,37 @@ def cpu_baseline(nbytes_total, bs, budget_s):
     return {"value": round(done / GiB / t_hash, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {done / GiB:.3f} GiB of the same splitmix64 stream, {bs}-B blocks, "
                       f"oracle/sf_oracle.c SHA-1 (scalar C, no SHA-NI), 1 thread, SQLite excluded"}
+
+
+def e2e_host_buffer(torch, data, dig_host, bs):
+    """End to end on the same bytes (not `value`): the shard copied to a host
+    buffer, then sf_index_buffer -- page-locked in place, pipelined H2D +
+    kernel + D2H of the rows -- best of two calls, rows checked against the
+    device-resident table.  Beside it the raw pinned H2D copy rate (the PCIe
+    ceiling of the route)."""
+    from syncfast_amd import host
+    hbytes = data.cpu().numpy()
+    best = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        rows = host.index_buffer(hbytes, bs)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    assert rows.shape[0] == dig_host.shape[0] and rows["sha1"].tobytes() == dig_host.tobytes(), "e2e rows differ"
+    n = hbytes.size
+    del hbytes, rows
+    pin = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(1 << 30, dtype=torch.uint8, device=data.device)
+    dev.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(4):
+        dev.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = (4 << 30) / (time.perf_counter() - t0)
+    return {"value": round(n / GiB / best, 3), "unit": "GiB/s", "gbs": round(n / best / 1e9, 2), "bytes": n,
+            "route": "host buffer -> sf_index_buffer (page-locked in place, pipelined H2D + kernel + D2H rows)",
+            "pcie_h2d_pinned_gbs": round(h2d / 1e9, 2)}
 
 
 def cpu_baseline_shani(nbytes_total, bs, budget_s, threads):
@@ -422,6 +458,9 @@ def main():
             traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
+    e2e = None
+    if not a.no_e2e and world == 1 and files is None and weaks is None:
+        e2e = e2e_host_buffer(torch, data, d, bs)
     cpu = cpu_all = cpu_ni = cpu_ni_all = None
     if not a.no_cpu_baseline and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
@@ -471,6 +510,7 @@ def main():
         "code_object_sha256": kernels,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
+        "e2e_host_buffer": e2e,
     }
     print(json.dumps(line), flush=True)
     if distributed:
