@@ -10,7 +10,7 @@
  *
  *   cc -O2 -I include examples/sf_index.c -L syncfast_amd/lib -lsyncfast_amd \
  *      -Wl,-rpath,$PWD/syncfast_amd/lib -o sf_index
- *   ./sf_index [-b block_size] path...
+ *   ./sf_index [-b block_size] [-m] path...      (-m: all paths through sf_index_files)
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -73,15 +73,42 @@ static int index_one(const char *path, uint32_t bs) {
     return rc;
 }
 
+/* -m: every path through ONE sf_index_files call (index_path's pipeline,
+ * src/index.rs:685-715), rows sized by a first call with cap 0. */
+static int index_many(char **paths, int n, uint32_t bs) {
+    uint64_t *first = malloc((n + 1) * sizeof(uint64_t)), need = 0;
+    uint8_t *hashes = malloc((size_t)n * 20);
+    uint32_t bad = 0;
+    if (!first || !hashes) return SF_ENOMEM;
+    int rc = sf_index_files((const char *const *)paths, (uint32_t)n, bs, 0, NULL, 0, first, hashes, &need, &bad);
+    sf_block_sig *rows = NULL;
+    if (rc == SF_ENOSPC || rc == SF_OK) {
+        rows = malloc((need ? need : 1) * sizeof(sf_block_sig));
+        rc = rows ? sf_index_files((const char *const *)paths, (uint32_t)n, bs, 0, rows, need, first, hashes, &need,
+                                   &bad)
+                  : SF_ENOMEM;
+    }
+    if (rc == SF_OK)
+        for (int k = 0; k < n; k++) print_rows(paths[k], rows + first[k], first[k + 1] - first[k], hashes + 20 * k);
+    else if (rc == SF_EIO)
+        fprintf(stderr, "%s: %s\n", paths[bad], sf_strerror(rc));
+    free(rows);
+    free(first);
+    free(hashes);
+    return rc;
+}
+
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
+    int many = 0;
     int i = 1;
-    if (i + 1 < argc && strcmp(argv[i], "-b") == 0) {
-        bs = (uint32_t)strtoul(argv[i + 1], NULL, 10);
-        i += 2;
+    for (; i < argc; i++) {
+        if (i + 1 < argc && strcmp(argv[i], "-b") == 0) bs = (uint32_t)strtoul(argv[++i], NULL, 10);
+        else if (strcmp(argv[i], "-m") == 0) many = 1;
+        else break;
     }
     if (i >= argc) {
-        fprintf(stderr, "usage: %s [-b block_size] path...\n", argv[0]);
+        fprintf(stderr, "usage: %s [-b block_size] [-m] path...\n", argv[0]);
         return 2;
     }
     int ndev = 0;
@@ -91,6 +118,11 @@ int main(int argc, char **argv) {
         return 1;
     }
     int status = 0;
+    if (many) {
+        status = index_many(argv + i, argc - i, bs) != SF_OK;
+        sf_release_host_cache();
+        return status;
+    }
     for (; i < argc; i++) {
         const int rc = index_one(argv[i], bs);
         if (rc != SF_OK) {

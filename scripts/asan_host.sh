@@ -1,0 +1,48 @@
+#!/bin/bash
+# Host-side AddressSanitizer run of the C-ABI's host pipelines on the GPU box:
+# the plain-C consumer (examples/sf_index.c) linked against a library whose
+# HOST code is ASan-instrumented (make -C examples asan; the GPU code is not),
+# over regular files (pread pipeline, small stages so many stage edges),
+# many files (sf_index_files), a FIFO and stdin (sf_index_fd).  Its output
+# must equal the uninstrumented build's, and ASan must report nothing.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+W=$(mktemp -d /tmp/sf_asan.XXXXXX)
+python3 - "$W" <<'EOF'
+import os, sys
+sys.path.insert(0, os.getcwd())
+import oracle
+w = sys.argv[1]
+sizes = [0, 1, 55, 56, 4095, 4096, 4097, 100_000, (5 << 20) + 77, (9 << 20) + 4096]
+for i, n in enumerate(sizes):
+    oracle.splitmix_bytes(n, 4000 + i).tofile(os.path.join(w, f"f{i:02d}"))
+for i in range(300):
+    oracle.splitmix_bytes((i * 7919) % 200_000, 5000 + i).tofile(os.path.join(w, f"s{i:03d}"))
+EOF
+export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:exitcode=99
+export SF_STREAM_STAGE_MIB=1
+rc=0
+run() {  # name cmd...  (both builds, same input, outputs compared)
+  local name=$1; shift
+  timeout -k 10 120 ./examples/build/sf_index "$@" > "$W/$name.plain" 2> "$W/$name.plain.err" < "$W/f07" || { echo "$name: plain build failed"; cat "$W/$name.plain.err"; return 1; }
+  timeout -k 10 300 ./examples/build/asan/sf_index "$@" > "$W/$name.asan" 2> "gpurun_out/asan_$name.err" < "$W/f07"
+  local r=$?
+  if [ $r -ne 0 ]; then echo "$name: asan build rc=$r"; tail -30 "gpurun_out/asan_$name.err"; return 1; fi
+  cmp -s "$W/$name.plain" "$W/$name.asan" || { echo "$name: outputs differ"; return 1; }
+  echo "$name: ok ($(wc -l < "$W/$name.asan") lines, asan clean)"
+}
+run files -b 4096 "$W"/f0* || rc=1
+run files_bs1000 -b 1000 "$W"/f0* || rc=1
+run many -m -b 4096 "$W"/s* "$W"/f0* || rc=1
+run stdin -b 4096 - || rc=1
+mkfifo "$W/pipe"
+( sleep 1; cat "$W/f08" > "$W/pipe" ) &
+timeout -k 10 120 ./examples/build/asan/sf_index -b 4096 "$W/pipe" > "$W/fifo.asan" 2> gpurun_out/asan_fifo.err
+r=$?; wait
+if [ $r -ne 0 ]; then echo "fifo: asan build rc=$r"; tail -30 gpurun_out/asan_fifo.err; rc=1
+else
+  ./examples/build/sf_index -b 4096 "$W/f08" | sed "s|$W/f08|$W/pipe|" > "$W/fifo.plain"
+  cmp -s "$W/fifo.plain" "$W/fifo.asan" && echo "fifo: ok (asan clean)" || { echo "fifo: outputs differ"; rc=1; }
+fi
+rm -rf "$W"
+exit $rc
