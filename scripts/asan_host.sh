@@ -20,6 +20,7 @@ for i in range(300):
     oracle.splitmix_bytes((i * 7919) % 200_000, 5000 + i).tofile(os.path.join(w, f"s{i:03d}"))
 EOF
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:exitcode=99
+export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1:exitcode=98
 export SF_STREAM_STAGE_MIB=1
 rc=0
 run() {  # name cmd...  (both builds, same input, outputs compared)
