@@ -546,7 +546,9 @@ int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* 
   // workspace, uploaded once.
   const bool need_table = !contiguous_aligned && total > 0;
   const bool need_fh = d_file_hashes != nullptr;
-  const size_t tbl_bytes = need_table ? total * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
+  // block table: offsets (u64) then sizes (u32), padded to 16 B so the file
+  // table's u64 offsets that follow stay 8-B aligned (host and device)
+  const size_t tbl_bytes = need_table ? (total * (sizeof(uint64_t) + sizeof(uint32_t)) + 15) & ~(size_t)15 : 0;
   const size_t fh_bytes = need_fh ? (size_t)n_files * (sizeof(uint64_t) + sizeof(uint32_t)) : 0;
   std::vector<uint8_t> host_ws(tbl_bytes + fh_bytes + 16);
   uint64_t* h_off = reinterpret_cast<uint64_t*>(host_ws.data());
