@@ -10,7 +10,9 @@
  *
  *   cc -O2 -I include examples/sf_index.c -L syncfast_amd/lib -lsyncfast_amd \
  *      -Wl,-rpath,$PWD/syncfast_amd/lib -o sf_index
- *   ./sf_index [-b block_size] [-m] path...      (-m: all paths through sf_index_files)
+ *   ./sf_index [-b block_size] [-m | -B | -s N] path...
+ *     -m: all paths through one sf_index_files call; -B: each file from a host
+ *     buffer (sf_index_buffer); -s N: each file as N sf_index_file_range shards
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -73,6 +75,47 @@ static int index_one(const char *path, uint32_t bs) {
     return rc;
 }
 
+/* -B: the file read into a host buffer, then sf_index_buffer (the in-place
+ * page-locked route from 1 MiB, the staged copy below); -s N: the file as N
+ * shards through sf_index_file_range, rows concatenated (the multi-GPU
+ * layout on one device), blocks_hash over all digests with sf_blocks_hash. */
+static int index_buffer_or_shards(const char *path, uint32_t bs, int shards) {
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;
+    const uint64_t len = (uint64_t)sb.st_size, nb = len ? (len + bs - 1) / bs : 0;
+    sf_block_sig *rows = malloc((nb ? nb : 1) * sizeof(sf_block_sig));
+    uint8_t *dig = malloc((nb ? nb : 1) * 20), bh[20];
+    uint64_t n = 0;
+    int rc = (rows && dig) ? SF_OK : SF_ENOMEM;
+    if (rc == SF_OK && shards <= 0) {
+        uint8_t *buf = malloc(len ? len : 1);
+        FILE *f = fopen(path, "rb");
+        if (!buf || !f || fread(buf, 1, len, f) != len) rc = SF_EIO;
+        if (f) fclose(f);
+        if (rc == SF_OK) rc = sf_index_buffer(buf, len, bs, rows, nb, &n);
+        free(buf);
+    } else if (rc == SF_OK) {
+        for (int r = 0; r < shards && rc == SF_OK; r++) {  /* shard_range: blocks dealt evenly */
+            const uint64_t per = nb / shards, extra = nb % shards;
+            const uint64_t ur = (uint64_t)r;
+            const uint64_t b0 = ur * per + (ur < extra ? ur : extra), cnt = per + (ur < extra ? 1 : 0);
+            const uint64_t start = b0 * bs < len ? b0 * bs : len;
+            const uint64_t end = (b0 + cnt) * bs < len ? (b0 + cnt) * bs : len;
+            uint64_t got = 0;
+            rc = sf_index_file_range(path, start, end - start, bs, rows + n, nb - n, &got);
+            n += got;
+        }
+    }
+    if (rc == SF_OK) {
+        for (uint64_t i = 0; i < n; i++) memcpy(dig + 20 * i, rows[i].sha1, 20);
+        rc = sf_blocks_hash(dig, n, bh);
+    }
+    if (rc == SF_OK) print_rows(path, rows, n, bh);
+    free(rows);
+    free(dig);
+    return rc;
+}
+
 /* -m: every path through ONE sf_index_files call (index_path's pipeline,
  * src/index.rs:685-715), rows sized by a first call with cap 0. */
 static int index_many(char **paths, int n, uint32_t bs) {
@@ -100,15 +143,17 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0;
+    int many = 0, buffer = 0, shards = 0;
     int i = 1;
     for (; i < argc; i++) {
         if (i + 1 < argc && strcmp(argv[i], "-b") == 0) bs = (uint32_t)strtoul(argv[++i], NULL, 10);
+        else if (i + 1 < argc && strcmp(argv[i], "-s") == 0) shards = atoi(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
+        else if (strcmp(argv[i], "-B") == 0) buffer = 1;
         else break;
     }
     if (i >= argc) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m] path...\n", argv[0]);
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path...\n", argv[0]);
         return 2;
     }
     int ndev = 0;
@@ -124,7 +169,8 @@ int main(int argc, char **argv) {
         return status;
     }
     for (; i < argc; i++) {
-        const int rc = index_one(argv[i], bs);
+        const int rc = (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)
+                                              : index_one(argv[i], bs);
         if (rc != SF_OK) {
             fprintf(stderr, "%s: %s\n", argv[i], sf_strerror(rc));
             status = 1;

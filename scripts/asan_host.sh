@@ -36,6 +36,11 @@ run files -b 4096 "$W"/f0* || rc=1
 run files_bs1000 -b 1000 "$W"/f0* || rc=1
 run many -m -b 4096 "$W"/s* "$W"/f0* || rc=1
 run stdin -b 4096 - || rc=1
+run buffer -B -b 4096 "$W"/f0* || rc=1
+run buffer_small -B -b 64 "$W"/f0[0-7] || rc=1
+run shards -s 3 -b 4096 "$W"/f0* || rc=1
+SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 run inplace -b 4096 "$W"/f0* || rc=1
+SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 SF_INPLACE_FAIL_AT=1 run inplace_bounce -b 4096 "$W"/f0* || rc=1
 mkfifo "$W/pipe"
 ( sleep 1; cat "$W/f08" > "$W/pipe" ) &
 timeout -k 10 120 ./examples/build/asan/sf_index -b 4096 "$W/pipe" > "$W/fifo.asan" 2> gpurun_out/asan_fifo.err
