@@ -41,6 +41,10 @@ run buffer_small -B -b 64 "$W"/f0[0-7] || rc=1
 run shards -s 3 -b 4096 "$W"/f0* || rc=1
 SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 run inplace -b 4096 "$W"/f0* || rc=1
 SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 SF_INPLACE_FAIL_AT=1 run inplace_bounce -b 4096 "$W"/f0* || rc=1
+# every route over the same files gives the same rows and blocks_hash
+for m in buffer shards inplace inplace_bounce; do
+  cmp -s "$W/files.asan" "$W/$m.asan" && echo "$m == files: ok" || { echo "$m differs from files"; rc=1; }
+done
 mkfifo "$W/pipe"
 ( sleep 1; cat "$W/f08" > "$W/pipe" ) &
 timeout -k 10 120 ./examples/build/asan/sf_index -b 4096 "$W/pipe" > "$W/fifo.asan" 2> gpurun_out/asan_fifo.err
