@@ -12,7 +12,8 @@
  *      -Wl,-rpath,$PWD/syncfast_amd/lib -o sf_index
  *   ./sf_index [-b block_size] [-m | -B | -s N] path...
  *     -m: all paths through one sf_index_files call; -B: each file from a host
- *     buffer (sf_index_buffer); -s N: each file as N sf_index_file_range shards
+ *     buffer (sf_index_buffer); -s N: each file as N sf_index_file_range shards;
+ *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -22,6 +23,11 @@
 #include <unistd.h>
 
 #include "syncfast_amd.h"
+
+/* -w only: device memory for the device-resident entry points (what a Rust
+ * binding would take from hip-sys). */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
 
 static void hex(const uint8_t *d, char out[41]) {
     static const char digits[] = "0123456789abcdef";
@@ -116,6 +122,26 @@ static int index_buffer_or_shards(const char *path, uint32_t bs, int shards) {
     return rc;
 }
 
+/* -w N: the device-resident path and the wire stream from C: N bytes of the
+ * splitmix64 stream (seed 0x5EED0000) generated in HBM
+ * (sf_fill_splitmix_device), hashed there (sf_index_device_fixed), and the
+ * file's FILE_BLOCK run (src/sync/ssh/proto.rs:162-166) streamed to stdout
+ * (sf_wire_file_blocks_fd). */
+static int wire_synthetic(uint64_t n, uint32_t bs) {
+    const uint64_t nb = n ? (n + bs - 1) / bs : 0;
+    void *d_data = NULL, *d_dig = NULL;
+    uint64_t got = 0, written = 0;
+    int rc = (hipMalloc(&d_data, n ? n : 1) == hipSuccess && hipMalloc(&d_dig, nb ? nb * 20 : 20) == hipSuccess)
+                 ? SF_OK : SF_ENOMEM;
+    if (rc == SF_OK) rc = sf_fill_splitmix_device(d_data, n, 0x5EED0000ull, 0, NULL);
+    if (rc == SF_OK) rc = sf_index_device_fixed(d_data, n, bs, d_dig, nb, &got, NULL);
+    if (rc == SF_OK) rc = sf_wire_file_blocks_fd(d_dig, nb, bs, n, 1, &written, NULL);
+    if (rc == SF_OK && written == 0 && nb) rc = SF_EIO;
+    if (d_data) (void)hipFree(d_data);
+    if (d_dig) (void)hipFree(d_dig);
+    return rc;
+}
+
 /* -m: every path through ONE sf_index_files call (index_path's pipeline,
  * src/index.rs:685-715), rows sized by a first call with cap 0. */
 static int index_many(char **paths, int n, uint32_t bs) {
@@ -144,16 +170,18 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0;
+    long long wire = -1;
     int i = 1;
     for (; i < argc; i++) {
         if (i + 1 < argc && strcmp(argv[i], "-b") == 0) bs = (uint32_t)strtoul(argv[++i], NULL, 10);
         else if (i + 1 < argc && strcmp(argv[i], "-s") == 0) shards = atoi(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-w") == 0) wire = atoll(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
         else break;
     }
-    if (i >= argc) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path...\n", argv[0]);
+    if (i >= argc && wire < 0) {
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path... | -w bytes\n", argv[0]);
         return 2;
     }
     int ndev = 0;
@@ -161,6 +189,12 @@ int main(int argc, char **argv) {
     if (ndev == 0) {
         fprintf(stderr, "%s: no HIP device (syncfast_amd has no CPU path)\n", argv[0]);
         return 1;
+    }
+    if (wire >= 0) {
+        const int rc = wire_synthetic((uint64_t)wire, bs);
+        if (rc != SF_OK) fprintf(stderr, "wire: %s\n", sf_strerror(rc));
+        sf_release_host_cache();
+        return rc != SF_OK;
     }
     int status = 0;
     if (many) {

@@ -76,3 +76,17 @@ def test_c_consumer_file_fifo_stdin(gpu, tmp_path):
         assert got[name]["rows"] == rows and got[name]["bh"] == bh, name
     r = subprocess.run([exe, str(tmp_path / "missing")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "I/O error" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bs", [(3 * 4096 + 5, 4096), (1 << 20, 65536), (0, 4096), (2_000_003, 1000)])
+def test_c_consumer_device_path_and_wire(gpu, n, bs):
+    # -w: bytes generated in HBM, hashed there and the FILE_BLOCK run streamed
+    # to stdout, all from C -- equal to write_message over the oracle's digests
+    from syncfast_amd import wire
+    from syncfast_amd.digest import HashDigest
+    r = subprocess.run([_built(False), "-w", str(n), "-b", str(bs)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    offs, sizes, dig = oracle.index_fixed(oracle.splitmix_bytes(n, 0x5EED0000), bs)
+    want = b"".join(wire.write_message("FileBlock", HashDigest(bytes(d)), int(s)) for d, s in zip(dig, sizes))
+    assert r.stdout == want
