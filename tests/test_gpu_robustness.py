@@ -145,3 +145,57 @@ def test_index_file_retries_when_the_file_grew(gpu, monkeypatch, tmp_path):
     offs, sizes, want = oracle.index_fixed(data, 4096)
     assert len(rows) == 6 and np.array_equal(np.stack([r["sha1"] for r in rows]), want)
     assert bh == oracle.blocks_hash(want)
+
+
+def test_concurrent_mixed_host_calls(gpu, tmp_path):
+    # the per-device cache under contention: six threads mixing buffer, file,
+    # fd, file-range and many-file calls (ctypes drops the GIL, so they run in
+    # parallel in the library) while a seventh releases the cache; every
+    # result equals the oracle's
+    import concurrent.futures as cf
+    bs = 4096
+    big = oracle.splitmix_bytes((48 << 20) + 999, 510)
+    small = [oracle.splitmix_bytes(n, 520 + i) for i, n in enumerate([0, 1, 5000, 70_000, 300_000])]
+    pb = tmp_path / "big"
+    big.tofile(pb)
+    ps = []
+    for i, d in enumerate(small):
+        p = tmp_path / f"s{i}"
+        d.tofile(p)
+        ps.append(p)
+    want_big = oracle.index_fixed(big, bs)[2]
+    want_small = [oracle.index_fixed(d, bs)[2] for d in small]
+
+    def job(kind):
+        torch.cuda.set_device(gpu)
+        for _ in range(4):
+            if kind == 0:
+                assert np.array_equal(host.index_buffer(big, bs)["sha1"], want_big)
+            elif kind == 1:
+                rows, bh = host.index_file(pb, bs)
+                assert np.array_equal(rows["sha1"], want_big) and bh == oracle.blocks_hash(want_big)
+            elif kind == 2:
+                fd = os.open(pb, os.O_RDONLY)
+                try:
+                    rows, bh = host.index_fd(fd, bs)
+                finally:
+                    os.close(fd)
+                assert np.array_equal(rows["sha1"], want_big)
+            elif kind == 3:
+                half = (big.size // 2) // bs * bs
+                a = host.index_file_range(pb, 0, half, bs)
+                b = host.index_file_range(pb, half, big.size - half, bs)
+                assert np.array_equal(np.concatenate([a, b])["sha1"], want_big)
+            elif kind == 4:
+                rows, first, fh = host.index_files(ps, bs)
+                for k, w in enumerate(want_small):
+                    assert np.array_equal(rows[int(first[k]):int(first[k + 1])]["sha1"].reshape(-1, 20), w)
+                    assert bytes(fh[k]) == oracle.blocks_hash(w)
+            elif kind == 5:
+                assert np.array_equal(host.index_buffer(small[3], bs)["sha1"].reshape(-1, 20), want_small[3])
+            else:
+                host.release_cache()
+        return kind
+
+    with cf.ThreadPoolExecutor(7) as ex:
+        assert sorted(ex.map(job, range(7))) == list(range(7))
