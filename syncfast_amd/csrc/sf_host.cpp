@@ -1,0 +1,709 @@
+// sf_host.cpp -- the C-ABI's host-memory entry points (include/syncfast_amd.h):
+// bytes in host memory, in a file or behind a descriptor -> pinned stages ->
+// H2D -> the gfx950 kernels (launched through sf_capi.hip) -> D2H of the rows,
+// plus the per-device cache of streams and buffers these calls share, the
+// streamed FILE_BLOCK run and the host SHA-1 helpers.  HIP runtime API only:
+// built with the host compiler.
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "host_sha1.h"
+#include "sf_internal.hpp"
+
+namespace sfi __attribute__((visibility("hidden"))) {
+std::mutex g_res_mu[kMaxDevices];
+HostRes* g_res[kMaxDevices];
+}  // namespace sfi
+
+using namespace sfi;
+
+namespace {
+
+// RAII pinned allocation (the in-place route's bounce buffer).
+struct PinBuf {
+  void* p = nullptr;
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+
+// Smallest host buffer / page-cache-resident file that sf_index_buffer /
+// sf_index_file copy in place (page-locked) instead of staging through the
+// pinned stages.  Per call, with the per-device set cached
+// (scripts/inplace_min_probe.py): a buffer gains in place from 1 MiB up
+// (7.6 vs 6.1 GB/s; 32 MiB: 45 vs 21); a file only from ~16 MiB (mapping and
+// locking page-cache pages loses to the 8-thread pread below 8 MiB: 4 MiB
+// 8.7 vs 10.3 GB/s; 32 MiB 24.3 vs 23.6).  SF_INPLACE_MIN_MIB overrides both
+// (A/B knob).
+inline uint64_t inplace_min_bytes(bool file) {
+  const char* e = getenv("SF_INPLACE_MIN_MIB");
+  const long v = e ? atol(e) : -1;
+  if (v >= 0) return (uint64_t)v << 20;
+  return file ? 16ull << 20 : 1ull << 20;
+}
+
+// Chunk of input handled per pipeline stage: a whole number of blocks, about
+// 256 MiB.
+inline uint64_t stage_bytes(uint32_t bs) {
+  const uint64_t target = 256ull << 20;
+  const uint64_t nb = std::max<uint64_t>(1, target / bs);
+  return nb * bs;
+}
+
+// Shared driver of sf_index_buffer / sf_index_file: `read(dst, off, n)`
+// fills a pinned staging buffer with input bytes [off, off+n).
+template <typename ReadFn>
+int index_pipelined(uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap, uint64_t* n_out, ReadFn read) {
+  const uint64_t nblocks = len ? ceil_div(len, bs) : 0;
+  if (n_out) *n_out = nblocks;
+  if (nblocks > cap) return SF_ENOSPC;
+  if (nblocks == 0) return SF_OK;
+  const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
+  const uint64_t nstages = ceil_div(len, stage);
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *pin[2], *ddig, *pdig;
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, stage, &ddata[i]);
+    if (rc == SF_OK) rc = res.pin(i, stage, &pin[i]);
+  }
+  if (rc == SF_OK) rc = res.dev(2, nblocks * 20, &ddig);
+  if (rc == SF_OK) rc = res.pin(2, nblocks * 20, &pdig);
+  if (rc != SF_OK) return rc;
+  for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    const uint64_t off = k * stage;
+    const uint64_t n = std::min(stage, len - off);
+    if (k >= 2) {
+      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    }
+    rc = read(static_cast<uint8_t*>(pin[b]), off, n);
+    if (rc != SF_OK) break;
+    if (hipMemcpyAsync(ddata[b], pin[b], n, hipMemcpyHostToDevice, st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    const uint64_t first_blk = off / bs;
+    const uint64_t nb = ceil_div(n, bs);
+    rc = launch_fixed(ddata[b], n, bs, nb, static_cast<uint8_t*>(ddig) + first_blk * 20, st[b]);
+    if (rc != SF_OK) break;
+    if (hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+  }
+  for (int i = 0; i < 2; i++)
+    if (hipStreamSynchronize(st[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipMemcpyAsync(pdig, ddig, nblocks * 20, hipMemcpyDeviceToHost, st[0]));
+  SF_HIP(hipStreamSynchronize(st[0]));
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig);
+  for (uint64_t i = 0; i < nblocks; i++) {
+    out[i].offset = i * bs;
+    out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
+    memcpy(out[i].sha1, dg + 20 * i, 20);
+  }
+  return SF_OK;
+}
+
+// In-place route of sf_index_buffer / sf_index_file: the DMA engine reads the
+// caller's pages (or the page-cache pages of a mapped file) directly, no
+// staging memcpy.  Per ~256 MiB stage, on alternating streams: H2D, the
+// block kernel, D2H of the stage's digests.  The host overlaps the rest with
+// the PCIe link:
+//   - the pages are page-locked (hipHostRegister) one region ahead of the
+//     copy that reads them, instead of all before the first copy;
+//   - stage k-1's rows are written and its digests folded into the file's
+//     blocks_hash (src/index.rs:661-682) while stage k is on the link.
+// Region k = [page_up(data + k*stage), page_up(data + (k+1)*stage)), so a
+// stage's bytes lie in regions k-1 (its head, up to the first page edge) and
+// k, and no page is registered twice.  A
+// region that cannot be registered after the first one switches the rest of
+// the stages to a pinned bounce buffer (memcpy, one stage at a time): slower,
+// same result.  For a mapped file (fd >= 0) the bounce buffer is filled
+// with pread from the fd, never by touching the mapping: a region that cannot
+// be page-locked is typically one past a concurrent truncation, and reading
+// the mapping there would raise SIGBUS; pread returns short instead, and the
+// call fails with SF_EIO (the reference's read() would see the short file).
+// Returns SF_ENOTSUP (nothing done) when the first region cannot be
+// registered, so the caller can take its staged route.
+// SF_INPLACE_SERIAL=1 registers the whole range first and writes rows and
+// blocks_hash after the last stage (the previous form; A/B knob).
+int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
+                         uint64_t* n_out, uint8_t* blocks_hash, int fd = -1) {
+  const uint64_t nblocks = ceil_div(len, bs);
+  if (n_out) *n_out = nblocks;
+  if (nblocks > cap) return SF_ENOSPC;
+  const char* ser = getenv("SF_INPLACE_SERIAL");
+  const bool serial = ser && atoi(ser);
+  const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
+  const uint64_t nstages = ceil_div(len, stage);
+  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t lo = (uintptr_t)data & ~(uintptr_t)(pg - 1);
+  const uintptr_t hi = ((uintptr_t)data + len + pg - 1) & ~(uintptr_t)(pg - 1);
+  auto edge = [&](uint64_t k) -> uintptr_t {  // start of region k (k = nstages: end of the range)
+    if (k == 0) return lo;
+    if (k >= nstages) return hi;
+    return std::min<uintptr_t>(hi, ((uintptr_t)data + k * stage + pg - 1) & ~(uintptr_t)(pg - 1));
+  };
+  enum { kEmpty, kLocked, kPageable, kPinned };  // kPinned: the caller's pages are already page-locked
+  std::vector<std::pair<void*, int>> regs;  // (region start, state)
+  struct Unreg {
+    std::vector<std::pair<void*, int>>* r;
+    ~Unreg() {
+      for (auto& x : *r)
+        if (x.second == kLocked) (void)hipHostUnregister(x.first);
+    }
+  } unreg{&regs};
+  // A buffer that is already page-locked (hipHostMalloc, or registered by the
+  // caller) is copied from as it is: hipHostRegister would refuse it.
+  auto pinned_at = [](const void* p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return at.type == hipMemoryTypeHost;
+  };
+  const bool prepinned = pinned_at(data) && pinned_at(data + len - 1);
+  const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to register
+  const long fail_k = fail_at ? atol(fail_at) : -1;
+  auto reg = [&](uint64_t k) {
+    const uintptr_t a = serial ? lo : edge(k), e = serial ? hi : edge(k + 1);
+    // after one failure every later region stays pageable (a stage straddles
+    // the page it shares with the previous region)
+    if (e <= a) { regs.push_back({(void*)a, kEmpty}); return; }
+    if (prepinned) { regs.push_back({(void*)a, kPinned}); return; }
+    if ((!regs.empty() && regs.back().second == kPageable) || (long)k == fail_k) {
+      regs.push_back({(void*)a, kPageable});
+      return;
+    }
+    const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
+    if (err != hipSuccess) (void)hipGetLastError();
+    regs.push_back({(void*)a, err == hipSuccess                               ? kLocked
+                              : err == hipErrorHostMemoryAlreadyRegistered ? kPinned
+                                                                           : kPageable});
+  };
+  reg(0);
+  if (regs[0].second != kLocked && regs[0].second != kPinned) return SF_ENOTSUP;
+  PinBuf bounce;  // only if a region after the first cannot be registered
+  HostLease res;  // declared after unreg and bounce: its release waits for the streams first
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *ddig, *pdig;
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) rc = res.dev(i, stage, &ddata[i]);
+  if (rc == SF_OK) rc = res.dev(2, nblocks * 20, &ddig);
+  if (rc == SF_OK) rc = res.pin(2, nblocks * 20, &pdig);
+  if (rc != SF_OK) return rc;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  const uint8_t* dg = static_cast<const uint8_t*>(pdig);
+  auto rows = [&](uint64_t k) {  // rows + blocks_hash of stage k (its digests are on the host)
+    const uint64_t b0 = k * stage / bs, b1 = std::min(nblocks, ceil_div((k + 1) * stage, bs));
+    for (uint64_t i = b0; i < b1; i++) {
+      out[i].offset = i * bs;
+      out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
+      memcpy(out[i].sha1, dg + 20 * i, 20);
+    }
+    if (blocks_hash) sf_host_sha1_update(&bh, dg + 20 * b0, (b1 - b0) * 20);
+  };
+  for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    const uint64_t off = k * stage;
+    const uint64_t n = std::min(stage, len - off);
+    const uint64_t b0 = off / bs, nb = ceil_div(n, bs);
+    uint8_t* dd = static_cast<uint8_t*>(ddig) + b0 * 20;
+    const uint8_t* src = data + off;
+    if (!serial && regs.back().second == kPageable) {  // region k is not page-locked: bounce
+      for (int i = 0; i < 2; i++)
+        if (hipStreamSynchronize(st[i]) != hipSuccess) rc = SF_ENODEV;
+      if (rc != SF_OK) break;
+      if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
+      if (fd >= 0) {
+        uint8_t* d = static_cast<uint8_t*>(bounce.p);
+        for (uint64_t got = 0; got < n && rc == SF_OK;) {
+          const ssize_t r = pread(fd, d + got, n - got, (off_t)(off + got));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) rc = SF_EIO;  // error, or the file shrank under us
+          else got += (uint64_t)r;
+        }
+        if (rc != SF_OK) break;
+      } else {
+        memcpy(bounce.p, src, n);
+      }
+      src = static_cast<const uint8_t*>(bounce.p);
+    }
+    // A copy must lie inside ONE registration: a stage that starts mid-page
+    // copies its head (up to the page edge, in region k-1) separately from
+    // the rest (region k).
+    const uint64_t head = (serial || src != data + off || k == 0) ? 0 : std::min<uint64_t>(n, edge(k) - (uintptr_t)src);
+    // stream b is in order: the copy into ddata[b] waits for the kernel of
+    // stage k-2 that read it.
+    if ((head && hipMemcpyAsync(ddata[b], src, head, hipMemcpyHostToDevice, st[b]) != hipSuccess) ||
+        (n > head && hipMemcpyAsync(static_cast<uint8_t*>(ddata[b]) + head, src + head, n - head,
+                                    hipMemcpyHostToDevice, st[b]) != hipSuccess)) {
+      rc = SF_ENODEV;
+      break;
+    }
+    rc = launch_fixed(ddata[b], n, bs, nb, dd, st[b]);
+    if (rc != SF_OK) break;
+    if (!serial) {
+      if (hipMemcpyAsync(static_cast<uint8_t*>(pdig) + b0 * 20, dd, nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+          hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+      if (k + 1 < nstages) reg(k + 1);
+      if (k >= 1) {
+        if (hipEventSynchronize(done[b ^ 1]) != hipSuccess) { rc = SF_ENODEV; break; }
+        rows(k - 1);
+      }
+    }
+  }
+  for (int i = 0; i < 2; i++)
+    if (hipStreamSynchronize(st[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  if (rc != SF_OK) return rc;
+  if (serial) {
+    SF_HIP(hipMemcpyAsync(pdig, ddig, nblocks * 20, hipMemcpyDeviceToHost, st[0]));
+    SF_HIP(hipStreamSynchronize(st[0]));
+    for (uint64_t k = 0; k < nstages; k++) rows(k);
+  } else {
+    rows(nstages - 1);
+  }
+  if (blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
+  return SF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sf_release_host_cache(void) {
+  for (int d = 0; d < kMaxDevices; d++) {
+    std::lock_guard<std::mutex> lk(g_res_mu[d]);  // waits for a call using the set
+    if (g_res[d]) {
+      g_res[d]->free_all();
+      delete g_res[d];
+      g_res[d] = nullptr;
+    }
+  }
+  return SF_OK;
+}
+
+#ifndef SF_WIRE_CHUNK_DEFAULT
+#define SF_WIRE_CHUNK_DEFAULT (1ull << 18)
+#endif
+static constexpr uint64_t kWireChunk = SF_WIRE_CHUNK_DEFAULT;  // messages per chunk (~9.4 MB at 4 KiB blocks)
+
+int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
+                           uint64_t* n_written, void* stream) {
+  if (n_written) *n_written = 0;
+  if (block_size == 0 || block_size > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
+  const uint64_t nb = file_len ? ceil_div(file_len, block_size) : 0;
+  if (nb != n_blocks) return SF_EINVAL;
+  if (!nb) return SF_OK;
+  if (!d_digests || fd < 0) return SF_EINVAL;
+  uint64_t db = 1;
+  for (uint64_t v = block_size; v >= 10; v /= 10) db++;
+  const uint32_t last = (uint32_t)(file_len - (nb - 1) * block_size);
+  uint64_t dl = 1;
+  for (uint64_t v = last; v >= 10; v /= 10) dl++;
+  const uint64_t msg = 33 + db;  // every message but the last
+  const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
+  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : kWireChunk);
+  const uint64_t nchunks = ceil_div(nb, per);
+  const uint64_t cap = std::min(per, nb) * msg + (33 + dl);
+  // Streams, events and the two chunk buffers (device + pinned) come from the
+  // per-device set the other host entry points keep between calls: pinning
+  // two chunk buffers per call cost more than the call's copies.
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* ev;
+  void *dout[2], *pin[2];
+  hipEvent_t ready = nullptr;
+  uint64_t bytes_of[2] = {0, 0};
+  int rc = res.streams(st, ev);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, cap, &dout[i]);
+    if (rc == SF_OK) rc = res.pin(i, cap, &pin[i]);
+  }
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  if (hipEventRecord(ready, as_stream(stream)) != hipSuccess ||  // the digests are produced on the caller's stream
+      hipStreamWaitEvent(st[0], ready, 0) != hipSuccess || hipStreamWaitEvent(st[1], ready, 0) != hipSuccess)
+    rc = SF_ENODEV;
+  uint64_t written = 0;
+  auto flush = [&](int b) {  // write chunk buffer b to fd, in order
+    if (hipEventSynchronize(ev[b]) != hipSuccess) return SF_ENODEV;
+    const uint8_t* p = static_cast<const uint8_t*>(pin[b]);
+    for (uint64_t done = 0; done < bytes_of[b];) {
+      const ssize_t w = write(fd, p + done, bytes_of[b] - done);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return SF_EIO;
+      done += (uint64_t)w;
+      written += (uint64_t)w;
+    }
+    return SF_OK;
+  };
+  // chunk k: device builds its messages, D2H into pin[k&1]; the host writes
+  // chunk k-2 while the device works on chunk k.
+  for (uint64_t k = 0; k < nchunks && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (k >= 2 && (rc = flush(b)) != SF_OK) break;
+    const uint64_t i0 = k * per, n = std::min(per, nb - i0);
+    const bool final_chunk = i0 + n == nb;
+    const uint32_t lsz = final_chunk ? last : block_size;
+    bytes_of[b] = (n - 1) * msg + (final_chunk ? 33 + dl : msg);
+    if (launch_wire(static_cast<const uint8_t*>(d_digests) + i0 * 20, n, block_size, lsz,
+                    static_cast<uint8_t*>(dout[b]), st[b]) != SF_OK ||
+        hipMemcpyAsync(pin[b], dout[b], bytes_of[b], hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(ev[b], st[b]) != hipSuccess)
+      rc = SF_ENODEV;
+  }
+  for (uint64_t k = nchunks >= 2 ? nchunks - 2 : 0; k < nchunks && rc == SF_OK; k++) rc = flush((int)(k & 1));
+  for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(st[i]);
+  (void)hipEventDestroy(ready);
+  if (n_written) *n_written = written;
+  return rc;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Staged file pipeline (sf_index_file's pread route and the sequential
+// route of sf_index_fd): two pinned stages of whole blocks (the last one
+// short).  `fill(dst, off, cap, &n, &eof)` puts the next input bytes into a
+// pinned stage; per stage, on alternating streams, H2D + block kernel + D2H of
+// the stage's digests.  While stage k is being filled, stage k-1 is on the
+// device and stage k-2's rows are emitted (`emit(first_block, n_blocks,
+// digests, stage_bytes)`) and its digests folded into the streaming
+// blocks_hash (src/index.rs:661-682), in order.  No device memory maps or
+// registers the caller's file: the host only ever reads it with read/pread.
+inline uint64_t file_stage_bytes(uint32_t bs) {
+  const char* se = getenv("SF_STREAM_STAGE_MIB");  // test knob: small stages exercise the pipeline
+  const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) << 20 : (256ull << 20);
+  return std::max<uint64_t>(1, want / bs) * bs;
+}
+
+template <typename FillFn, typename EmitFn>
+int staged_pipeline(uint32_t bs, uint64_t stage, FillFn fill, EmitFn emit, uint8_t* blocks_hash) {
+  const uint64_t sblocks = stage / bs;
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *pin[2], *ddig[2], *pdig[2];
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, stage, &ddata[i]);
+    if (rc == SF_OK) rc = res.pin(i, stage, &pin[i]);
+    if (rc == SF_OK) rc = res.dev(3 + i, sblocks * 20, &ddig[i]);
+    if (rc == SF_OK) rc = res.pin(3 + i, sblocks * 20, &pdig[i]);
+  }
+  if (rc != SF_OK) return rc;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  uint64_t bytes_of[2] = {0, 0}, first_of[2] = {0, 0};
+  bool busy[2] = {false, false};
+  auto harvest = [&](int b) {
+    if (hipEventSynchronize(done[b]) != hipSuccess) return SF_ENODEV;
+    busy[b] = false;
+    const uint64_t nb = ceil_div(bytes_of[b], bs);
+    const uint8_t* dg = static_cast<const uint8_t*>(pdig[b]);
+    const int r = emit(first_of[b], nb, dg, bytes_of[b]);
+    if (r != SF_OK) return r;
+    if (blocks_hash) sf_host_sha1_update(&bh, dg, nb * 20);
+    return SF_OK;
+  };
+  uint64_t total = 0;
+  bool eof = false;
+  for (uint64_t k = 0; !eof && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (busy[b] && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (stage k-1 is later in file order)
+    uint8_t* dst = static_cast<uint8_t*>(pin[b]);
+    uint64_t n = 0;
+    if ((rc = fill(dst, total, stage, &n, &eof)) != SF_OK || n == 0) break;
+    const uint64_t nb = ceil_div(n, bs);
+    bytes_of[b] = n;
+    first_of[b] = total / bs;  // every earlier stage was whole blocks
+    total += n;
+    if (hipMemcpyAsync(ddata[b], dst, n, hipMemcpyHostToDevice, st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    if ((rc = launch_fixed(ddata[b], n, bs, nb, ddig[b], st[b])) != SF_OK) break;
+    if (hipMemcpyAsync(pdig[b], ddig[b], nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+    busy[b] = true;
+  }
+  // the (at most two) stages still in flight, in file order
+  int order[2] = {0, 1};
+  if (busy[0] && busy[1] && first_of[1] < first_of[0]) std::swap(order[0], order[1]);
+  for (int b : order)
+    if (busy[b]) {
+      const int r = harvest(b);
+      if (rc == SF_OK) rc = r;
+    }
+  if (rc == SF_OK && blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
+  return rc;
+}
+
+// Rows in a growing malloc'd buffer (sf_index_fd; the sequential route of
+// sf_index_file).
+struct RowBuf {
+  sf_block_sig* p = nullptr;
+  uint64_t n = 0, cap = 0;
+  ~RowBuf() { free(p); }
+  bool grow(uint64_t need) {
+    if (need <= cap) return true;
+    uint64_t c = std::max<uint64_t>({need, 2 * cap, 1024});
+    void* q = realloc(p, c * sizeof(sf_block_sig));
+    if (!q) return false;
+    p = static_cast<sf_block_sig*>(q);
+    cap = c;
+    return true;
+  }
+  sf_block_sig* release() {
+    sf_block_sig* q = p;
+    p = nullptr;
+    n = cap = 0;
+    return q;
+  }
+};
+
+inline void write_rows(sf_block_sig* o, uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes, uint32_t bs) {
+  for (uint64_t i = 0; i < nb; i++) {
+    o[i].offset = (first + i) * bs;
+    o[i].size = (uint32_t)std::min<uint64_t>(bs, bytes - i * bs);
+    memcpy(o[i].sha1, dg + 20 * i, 20);
+  }
+}
+
+// Sequential route (input that cannot seek: a pipe, FIFO, socket or
+// character device -- what index_file's File::open + read accepts,
+// src/index.rs:615,625): read() to EOF.
+static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash) {
+  auto fill = [&](uint8_t* dst, uint64_t, uint64_t cap, uint64_t* n, bool* eof) {
+    *n = 0;
+    while (*n < cap) {
+      const ssize_t r = read(fd, dst + *n, cap - *n);
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) return SF_EIO;
+      if (r == 0) { *eof = true; break; }
+      *n += (uint64_t)r;
+    }
+    return SF_OK;
+  };
+  auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
+    if (!rows.grow(rows.n + nb)) return SF_ENOMEM;
+    write_rows(rows.p + rows.n, first, nb, dg, bytes, bs);
+    rows.n += nb;
+    return SF_OK;
+  };
+  return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
+}
+
+// Regular file of known length: each stage is read by several threads in
+// parallel (one pread stream per slice; one thread copies from the page
+// cache at ~16 GB/s, below PCIe).  A short read (the file shrank) is SF_EIO.
+// Read-ahead (SF_FADVISE, default on): the file is declared sequential and,
+// before stage k is read, the kernel is asked to start fetching stage k+1
+// (POSIX_FADV_WILLNEED), so a file that is not in the page cache streams from
+// the disk while stage k is copied; for a resident file both are no-ops.
+inline bool fadvise_on() {
+  const char* e = getenv("SF_FADVISE");
+  return !e || atoi(e) != 0;
+}
+
+// Bytes [base, base + len) of the file (base a multiple of bs: a shard of
+// one logical file); row offsets are file offsets.
+static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf_block_sig* out,
+                            uint8_t* blocks_hash) {
+  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
+  const bool adv = fadvise_on();
+  if (adv) (void)posix_fadvise(fd, (off_t)base, (off_t)len, POSIX_FADV_SEQUENTIAL);
+  auto fill = [&](uint8_t* dst, uint64_t off, uint64_t cap, uint64_t* nout, bool* eof) {
+    const uint64_t n = std::min(cap, len - off);
+    *nout = n;
+    *eof = off + n >= len;
+    if (adv && !*eof)
+      (void)posix_fadvise(fd, (off_t)(base + off + n), (off_t)std::min(cap, len - off - n), POSIX_FADV_WILLNEED);
+    auto read_slice = [&](uint64_t a, uint64_t b) {
+      for (uint64_t got = a; got < b;) {
+        const ssize_t r = pread(fd, dst + got, b - got, (off_t)(base + off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return SF_EIO;
+        got += (uint64_t)r;
+      }
+      return SF_OK;
+    };
+    const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
+    std::vector<std::thread> pool;
+    std::vector<int> rcs(nthreads, SF_OK);
+    for (unsigned t = 1; t < nthreads && t * slice < n; t++)
+      pool.emplace_back([&, t] { rcs[t] = read_slice(t * slice, std::min(n, (t + 1) * slice)); });
+    rcs[0] = read_slice(0, std::min(n, slice));
+    for (auto& th : pool) th.join();
+    for (int r : rcs)
+      if (r) return r;
+    return SF_OK;
+  };
+  auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
+    write_rows(out + first, base / bs + first, nb, dg, bytes, bs);
+    return SF_OK;
+  };
+  return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
+                    uint64_t* n_out) {
+  int rc = check_fixed_args(len, block_size);
+  if (rc) return rc;
+  if (len && (!data || !out)) return SF_EINVAL;
+  // Large buffers: page-lock in place (no staging memcpy); SF_NO_HOSTREG=1
+  // forces the staged path (A/B knob).
+  const char* noreg = getenv("SF_NO_HOSTREG");
+  if (len && len >= inplace_min_bytes(false) && !(noreg && atoi(noreg))) {
+    rc = index_inplace(data, len, block_size, out, cap, n_out, nullptr);
+    if (rc != SF_ENOTSUP) return rc;
+  }
+  return index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
+    memcpy(dst, data + off, n);
+    return SF_OK;
+  });
+}
+
+int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
+                  uint8_t blocks_hash[20]) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (!path) return SF_EINVAL;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return SF_EIO;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || S_ISDIR(sb.st_mode)) { close(fd); return SF_EIO; }
+  if (!S_ISREG(sb.st_mode)) {
+    // Not seekable (FIFO, socket, character device): the sequential route.
+    // The input is consumed, so with too small a cap the rows are lost and
+    // SF_ENOSPC reports the need (sf_index_fd has no cap to miss).
+    RowBuf rows;
+    uint8_t bh[20];
+    rc = index_stream(fd, block_size, rows, bh);
+    close(fd);
+    if (rc != SF_OK) return rc;
+    if (n_out) *n_out = rows.n;
+    if (rows.n > cap) return SF_ENOSPC;
+    if (rows.n && !out) return SF_EINVAL;
+    if (rows.n) memcpy(out, rows.p, rows.n * sizeof(sf_block_sig));
+    if (blocks_hash) memcpy(blocks_hash, bh, 20);
+    return SF_OK;
+  }
+  const off_t end = lseek(fd, 0, SEEK_END);
+  if (end < 0) { close(fd); return SF_EIO; }
+  const uint64_t len = (uint64_t)end;
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_out) *n_out = nb;
+  if (nb > cap) { close(fd); return SF_ENOSPC; }
+  if (nb && !out) { close(fd); return SF_EINVAL; }
+  // Opt-in (SF_FILE_INPLACE=1): a large file already in the page cache is
+  // mapped and the mapping page-locked in place (hipHostRegister), so the DMA
+  // engine reads the page-cache pages directly -- no pread copy (the in-place
+  // path of sf_index_buffer).  Not the default: a registered file mapping is
+  // a GPU userptr, and a concurrent truncation of the file invalidates it
+  // under the in-flight copies -- measured on MI355X, the process's queues
+  // then never resume and the call hangs (tests/test_gpu_robustness.py).  The
+  // default pread pipeline only ever reads the file, so a file that shrinks
+  // mid-call gives SF_EIO, like the short read the reference would see.
+  const char* inpl = getenv("SF_FILE_INPLACE");
+  if (len && len >= inplace_min_bytes(true) && inpl && atoi(inpl)) {
+    void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
+    if (m != MAP_FAILED) {
+      const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+      std::vector<unsigned char> res(ceil_div(len, pg));
+      uint64_t resident = 0;
+      if (mincore(m, len, res.data()) == 0)
+        for (unsigned char r : res) resident += r & 1u;
+      if (resident * 10 >= res.size() * 9) {
+        rc = index_inplace(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out, blocks_hash, fd);
+        if (rc != SF_ENOTSUP) {
+          munmap(m, len);
+          close(fd);
+          return rc;
+        }
+      }
+      munmap(m, len);
+    }
+  }
+  if (nb == 0) {
+    close(fd);
+    static const uint8_t none = 0;
+    if (blocks_hash) sf_host_sha1_impl(&none, 0, blocks_hash, 0);
+    return SF_OK;
+  }
+  rc = index_file_pread(fd, 0, len, block_size, out, blocks_hash);
+  close(fd);
+  return rc;
+}
+
+int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t block_size, sf_block_sig* out,
+                        uint64_t cap, uint64_t* n_out) {
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (!path || (len && start % block_size)) return SF_EINVAL;  // an empty shard may start anywhere up to EOF
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_out) *n_out = nb;
+  if (nb > cap) return SF_ENOSPC;
+  if (nb && !out) return SF_EINVAL;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return SF_EIO;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return SF_EIO; }
+  if (start > (uint64_t)sb.st_size || len > (uint64_t)sb.st_size - start) { close(fd); return SF_ERANGE; }
+  rc = nb ? index_file_pread(fd, start, len, block_size, out, nullptr) : SF_OK;
+  close(fd);
+  return rc;
+}
+
+int sf_index_fd(int fd, uint32_t block_size, sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[20]) {
+  if (rows) *rows = nullptr;
+  if (n_out) *n_out = 0;
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (fd < 0 || !rows || !n_out) return SF_EINVAL;
+  RowBuf rb;
+  rc = index_stream(fd, block_size, rb, blocks_hash);
+  if (rc != SF_OK) return rc;
+  *n_out = rb.n;
+  *rows = rb.release();
+  return SF_OK;
+}
+
+void sf_free_rows(sf_block_sig* rows) { free(rows); }
+
+int sf_sha1_host(const uint8_t* data, uint64_t len, uint8_t out[20]) {
+  if (!out || (len && !data)) return SF_EINVAL;
+  sf_host_sha1_impl(data, len, out, 0);
+  return SF_OK;
+}
+
+int sf_blocks_hash(const uint8_t* digests, uint64_t n, uint8_t out[20]) {
+  if (!out || (n && !digests)) return SF_EINVAL;
+  sf_host_sha1_impl(digests, n * 20, out, 0);
+  return SF_OK;
+}
+
+int sf_blocks_hash_sigs(const sf_block_sig* sigs, uint64_t n, uint8_t out[20]) {
+  if (!out || (n && !sigs)) return SF_EINVAL;
+  // Gather the digests into one contiguous run (AoS rows are 32 B apart).
+  std::vector<uint8_t> buf(n * 20);
+  for (uint64_t i = 0; i < n; i++) memcpy(buf.data() + 20 * i, sigs[i].sha1, 20);
+  sf_host_sha1_impl(buf.data(), n * 20, out, 0);
+  return SF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,179 @@
+// sf_internal.hpp -- library-internal declarations shared by the C-ABI's
+// translation units (not part of include/syncfast_amd.h):
+//   sf_capi.hip   the gfx950 kernels' launchers and the device-resident entry
+//                 points (the only TU compiled for the GPU);
+//   sf_host.cpp   the host-memory entry points: per-device cache of streams
+//                 and staging buffers, the buffer / file / fd / range
+//                 pipelines, the wire stream, host SHA-1 helpers;
+//   sf_files.cpp  sf_index_files, the many-file pipeline.
+// The .cpp files use only the HIP runtime API (no kernels), so they build
+// with the host compiler.
+#pragma once
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/syncfast_amd.h"
+
+// Internal status of the in-place route (never returned through the C-ABI):
+// the caller's pages could not be page-locked, take the staged route.
+#define SF_ENOTSUP (-95)
+
+#define SF_HIP(call)                       \
+  do {                                     \
+    hipError_t _e = (call);                \
+    if (_e != hipSuccess) return sfi::hip_err(_e); \
+  } while (0)
+
+namespace sfi __attribute__((visibility("hidden"))) {
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int hip_err(hipError_t e) {
+  if (e == hipSuccess) return SF_OK;
+  if (e == hipErrorOutOfMemory) return SF_ENOMEM;
+  return SF_ENODEV;
+}
+
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+inline int check_fixed_args(uint64_t len, uint32_t bs) {
+  if (bs == 0 || bs > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
+  (void)len;
+  return SF_OK;
+}
+
+// Launchers of the gfx950 kernels (sf_capi.hip).
+int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
+                 hipStream_t stream, uint32_t* weak = nullptr);
+int launch_wire(const uint8_t* d_digests, uint64_t n, uint32_t bs, uint32_t last, uint8_t* d_out,
+                hipStream_t stream);
+
+// Per-device resources of the host-memory entry points (streams, events,
+// device stage buffers, digest table, pinned stages), kept between calls:
+// setting them up cost ~8 ms per call (hipMalloc / hipHostMalloc of the
+// stages), ten times the PCIe time of a 64 MiB file.  One call at a time uses
+// a device's set; a concurrent call gets a private set.  Capacities only
+// grow, up to kCacheMax per buffer; a larger buffer is allocated for the call
+// alone.  sf_release_host_cache() frees the sets.  They are never freed from
+// a static destructor: the HIP runtime may already be gone at exit.
+constexpr uint64_t kCacheMax = 512ull << 20;
+constexpr int kMaxDevices = 64;
+
+struct HostRes {
+  hipStream_t s[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  // Slots (device and pinned alike): 0, 1 = the two stages; 2 = the digest
+  // table of one file; 3, 4 = the digest tables of sf_index_files' two
+  // stages; 5, 6 = their blocks_hash arrays; 7 = their status words.
+  static constexpr int kSlots = 8;
+  void* dev[kSlots] = {};
+  uint64_t dev_cap[kSlots] = {};
+  void* pin[kSlots] = {};
+  uint64_t pin_cap[kSlots] = {};
+  void free_all() {
+    for (int i = 0; i < kSlots; i++) {
+      if (dev[i]) (void)hipFree(dev[i]);
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      dev[i] = pin[i] = nullptr;
+      dev_cap[i] = pin_cap[i] = 0;
+    }
+    for (int i = 0; i < 2; i++) {
+      if (s[i]) (void)hipStreamDestroy(s[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      s[i] = nullptr;
+      ev[i] = nullptr;
+    }
+  }
+};
+
+// Defined in sf_host.cpp.
+extern std::mutex g_res_mu[kMaxDevices];
+extern HostRes* g_res[kMaxDevices];
+
+class HostLease {
+ public:
+  HostLease() {
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices) {
+      lk_ = std::unique_lock<std::mutex>(g_res_mu[d], std::try_to_lock);
+      if (lk_.owns_lock()) {
+        if (!g_res[d]) g_res[d] = new HostRes;
+        r_ = g_res[d];
+        return;
+      }
+    } else {
+      (void)hipGetLastError();
+    }
+    own_ = new HostRes;
+    r_ = own_;
+  }
+  ~HostLease() {
+    for (int i = 0; i < 2; i++)  // an early error return may leave copies in flight
+      if (r_->s[i]) (void)hipStreamSynchronize(r_->s[i]);
+    for (void* p : tmp_dev_) (void)hipFree(p);
+    for (void* p : tmp_pin_) (void)hipHostFree(p);
+    if (own_) {
+      own_->free_all();
+      delete own_;
+    }
+  }
+  HostLease(const HostLease&) = delete;
+  HostLease& operator=(const HostLease&) = delete;
+  int streams(hipStream_t*& s, hipEvent_t*& ev) {
+    for (int i = 0; i < 2; i++) {
+      if (!r_->s[i]) SF_HIP(hipStreamCreateWithFlags(&r_->s[i], hipStreamNonBlocking));
+      if (!r_->ev[i]) SF_HIP(hipEventCreateWithFlags(&r_->ev[i], hipEventDisableTiming));
+    }
+    s = r_->s;
+    ev = r_->ev;
+    return SF_OK;
+  }
+  int dev(int i, uint64_t need, void** out) { return get(r_->dev[i], r_->dev_cap[i], need, false, out); }
+  int pin(int i, uint64_t need, void** out) { return get(r_->pin[i], r_->pin_cap[i], need, true, out); }
+
+ private:
+  int get(void*& slot, uint64_t& cap, uint64_t need, bool pinned, void** out) {
+    need = std::max<uint64_t>(need, 1);
+    if (need <= cap) {
+      *out = slot;
+      return SF_OK;
+    }
+    void* p = nullptr;
+    if (pinned) SF_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
+    else SF_HIP(hipMalloc(&p, need));
+    if (need > kCacheMax) {
+      (pinned ? tmp_pin_ : tmp_dev_).push_back(p);
+    } else {
+      if (slot) (void)(pinned ? hipHostFree(slot) : hipFree(slot));
+      slot = p;
+      cap = need;
+    }
+    *out = p;
+    return SF_OK;
+  }
+  std::unique_lock<std::mutex> lk_;
+  HostRes* r_ = nullptr;
+  HostRes* own_ = nullptr;
+  std::vector<void*> tmp_dev_, tmp_pin_;
+};
+
+// Reader threads of the pread routes (sf_index_file, sf_index_files).
+// SF_IO_THREADS overrides the default of 16 (A/B knob).  With the stat phase
+// parallel too, 16 readers beat 8 on many small files (10,537 files of
+// 0-200 KiB: 29.3 vs 24.1 GB/s, 12 and 24 no better; 8 MiB files flat at
+// 33-34 GB/s; profiles/r02/e2e/io_threads_8_12_16_24.log).
+inline unsigned io_threads() {
+  const char* e = getenv("SF_IO_THREADS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? (unsigned)std::min(v, 64) : 16u;
+}
+
+}  // namespace sfi
