@@ -9,7 +9,11 @@ Modules
   host    -- host-memory / file entry points (end-to-end, incl. H2D/D2H)
   digest  -- HashDigest, the signature value type (src/lib.rs:72-145)
   index   -- Index, the reference's library API on SQLite (src/index.rs)
-  shard   -- multi-GPU sharding + RCCL gather of the signature table
+  timestamp -- files.modified as chrono's DateTime<Utc> (src/index.rs:176-218)
+  shard   -- multi-GPU sharding + RCCL gather of the signature table, and one
+             file on disk indexed by every rank
+  wire    -- FILE_BLOCK / FILE_ENTRY framing (src/sync/ssh/proto.rs) and the
+             device-built FILE_BLOCK run
 """
 from ._lib import (HASH_DIGEST_LEN, LIB_PATH, MAX_BLOCK_SIZE, SfError, device_count,  # noqa: F401
                    lib)
