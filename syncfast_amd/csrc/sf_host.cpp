@@ -25,61 +25,6 @@
 namespace sfi __attribute__((visibility("hidden"))) {
 std::mutex g_res_mu[kMaxDevices];
 HostRes* g_res[kMaxDevices];
-
-namespace {
-struct ThpBlock {
-  void* base;  // the mapping
-  size_t len;
-};
-std::mutex g_thp_mu;
-std::vector<std::pair<void*, ThpBlock>> g_thp;  // aligned pointer -> mapping
-
-bool pin_thp() {
-  static const int on = [] {
-    const char* e = getenv("SF_PIN_THP");
-    return e && atoi(e) ? 1 : 0;
-  }();
-  return on;
-}
-}  // namespace
-
-int pin_alloc(void** p, uint64_t n) {
-  *p = nullptr;
-  if (!pin_thp()) return hip_err(hipHostMalloc(p, n, hipHostMallocDefault));
-  constexpr size_t kHuge = 2u << 20;
-  const size_t len = ((size_t)n + kHuge - 1) / kHuge * kHuge + kHuge;
-  void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-  if (m == MAP_FAILED) return SF_ENOMEM;
-  void* a = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(m) + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
-  (void)madvise(a, len - kHuge, MADV_HUGEPAGE);
-  memset(a, 0, len - kHuge);  // fault the huge pages in before locking them
-  const hipError_t e = hipHostRegister(a, len - kHuge, hipHostRegisterDefault);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    munmap(m, len);
-    return hip_err(e);
-  }
-  std::lock_guard<std::mutex> lk(g_thp_mu);
-  g_thp.push_back({a, {m, len}});
-  *p = a;
-  return SF_OK;
-}
-
-void pin_free(void* p) {
-  if (!p) return;
-  {
-    std::lock_guard<std::mutex> lk(g_thp_mu);
-    for (size_t i = 0; i < g_thp.size(); i++)
-      if (g_thp[i].first == p) {
-        const ThpBlock b = g_thp[i].second;
-        g_thp.erase(g_thp.begin() + (long)i);
-        (void)hipHostUnregister(p);
-        munmap(b.base, b.len);
-        return;
-      }
-  }
-  (void)hipHostFree(p);
-}
 }  // namespace sfi
 
 using namespace sfi;
@@ -89,7 +34,7 @@ namespace {
 // RAII pinned allocation (the in-place route's bounce buffer).
 struct PinBuf {
   void* p = nullptr;
-  ~PinBuf() { pin_free(p); }
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
 };
 
 // Smallest host buffer / page-cache-resident file that sf_index_buffer /
@@ -280,7 +225,7 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
       for (int i = 0; i < 2; i++)
         if (hipStreamSynchronize(st[i]) != hipSuccess) rc = SF_ENODEV;
       if (rc != SF_OK) break;
-      if (!bounce.p && (rc = pin_alloc(&bounce.p, stage)) != SF_OK) break;
+      if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
       if (fd >= 0) {
         uint8_t* d = static_cast<uint8_t*>(bounce.p);
         for (uint64_t got = 0; got < n && rc == SF_OK;) {

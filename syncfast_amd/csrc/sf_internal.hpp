@@ -50,12 +50,6 @@ inline int check_fixed_args(uint64_t len, uint32_t bs) {
   return SF_OK;
 }
 
-// Page-locked host staging memory (sf_host.cpp): hipHostMalloc, or with
-// SF_PIN_THP=1 (A/B knob) anonymous memory backed by transparent huge pages
-// and page-locked with hipHostRegister.  pin_free takes either kind.
-int pin_alloc(void** p, uint64_t n);
-void pin_free(void* p);
-
 // Launchers of the gfx950 kernels (sf_capi.hip).
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
                  hipStream_t stream, uint32_t* weak = nullptr);
@@ -87,7 +81,7 @@ struct HostRes {
   void free_all() {
     for (int i = 0; i < kSlots; i++) {
       if (dev[i]) (void)hipFree(dev[i]);
-      if (pin[i]) pin_free(pin[i]);
+      if (pin[i]) (void)hipHostFree(pin[i]);
       dev[i] = pin[i] = nullptr;
       dev_cap[i] = pin_cap[i] = 0;
     }
@@ -125,7 +119,7 @@ class HostLease {
     for (int i = 0; i < 2; i++)  // an early error return may leave copies in flight
       if (r_->s[i]) (void)hipStreamSynchronize(r_->s[i]);
     for (void* p : tmp_dev_) (void)hipFree(p);
-    for (void* p : tmp_pin_) pin_free(p);
+    for (void* p : tmp_pin_) (void)hipHostFree(p);
     if (own_) {
       own_->free_all();
       delete own_;
@@ -153,18 +147,12 @@ class HostLease {
       return SF_OK;
     }
     void* p = nullptr;
-    if (pinned) {
-      const int rc = pin_alloc(&p, need);
-      if (rc != SF_OK) return rc;
-    }
+    if (pinned) SF_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
     else SF_HIP(hipMalloc(&p, need));
     if (need > kCacheMax) {
       (pinned ? tmp_pin_ : tmp_dev_).push_back(p);
     } else {
-      if (slot) {
-        if (pinned) pin_free(slot);
-        else (void)hipFree(slot);
-      }
+      if (slot) (void)(pinned ? hipHostFree(slot) : hipFree(slot));
       slot = p;
       cap = need;
     }
