@@ -2,7 +2,10 @@
 memory on transparent huge pages, page-locked with hipHostRegister
 (SF_PIN_THP=1).  The knob is read once per process, so each setting runs in
 its own child process, alternating: the page-cache copy into the stages
-(pread) and the DMA out of them are what changes.
+(pread) and the DMA out of them are what changes.  Result
+(profiles/r02/e2e/thp_pinned_ab.log): no gain, so the knob was removed from
+the library after the run (commit "Remove the THP staging knob"); run as is,
+both settings now measure the default.
 
 usage: python scripts/thp_probe.py            (parent: writes inputs, runs children)
        python scripts/thp_probe.py child DIR  (one measurement set)"""
