@@ -150,6 +150,24 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
 }
 
+#ifndef SF_SCALAR_ISSUE
+#define SF_SCALAR_ISSUE 0  // 1: span base/length made uniform once, per-step resource math in SALU (A/B)
+#endif
+// The same DMA step with the span base and length already in SGPRs (hoisted
+// out of the step loop): the per-step resource arithmetic is scalar.
+template <int TILE>
+__device__ __forceinline__ void issue_step_s(uint64_t ptr_s, uint64_t span_s, uint32_t step, const uint32_t* voff,
+                                             uint4* wave_tile) {
+  const uint64_t toff = (uint64_t)step * TILE;
+  const uint64_t left = span_s > toff ? span_s - toff : 0;
+  const uint32_t nrec = left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left;
+  __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr_s + toff), (short)0, (int)nrec, (int)kRsrcWord3);
+#pragma unroll
+  for (int j = 0; j < TILE / 16; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
+}
+
 // Hash the block (off, size) owned by this lane; all 64 lanes of the wave
 // enter together.  `rel` = off - geo.base (valid lanes).  TILE = bytes of
 // each block staged per LDS step.  WEAK: also fold the same words into the
@@ -189,7 +207,14 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     const uint4* my = wave_tile + lane * PIECES;
     const uint8_t* span_ptr = data + geo.base;
 
-    if (nsteps > 0) issue_step<TILE>(span_ptr, geo.span, 0, voff, wave_tile);
+#if SF_SCALAR_ISSUE
+    const uint64_t ptr_s = uniform_u64(reinterpret_cast<uint64_t>(span_ptr));
+    const uint64_t span_s = uniform_u64(geo.span);
+#define SF_ISSUE(step) issue_step_s<TILE>(ptr_s, span_s, (step), voff, wave_tile)
+#else
+#define SF_ISSUE(step) issue_step<TILE>(span_ptr, geo.span, (step), voff, wave_tile)
+#endif
+    if (nsteps > 0) SF_ISSUE(0);
     for (uint32_t t = 0; t < nsteps; ++t) {
       uint4 raw[PIECES];
 #ifndef SF_EXPERIMENT_NOLOAD
@@ -202,7 +227,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
       // chunk 0's compression, and the next DMA is issued after it.
 #else
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t + 1 < nsteps) issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+      if (t + 1 < nsteps) SF_ISSUE(t + 1);
 #endif
 #else
       // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_NOLOAD):
@@ -219,7 +244,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
           // unconditional (no branch in the loop body): past the last step
           // the resource has num_records 0, every lane reads zeros, nobody
           // reads the tile again.
-          issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
+          SF_ISSUE(t + 1);
         }
 #endif
         uint32_t w[16];
@@ -246,6 +271,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
         st.compress(w);
       }
     }
+#undef SF_ISSUE
     c_done = nsteps * CH;
   } else {
     // Misaligned or > 4 GiB span: each lane streams its own block.
