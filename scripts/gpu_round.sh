@@ -28,6 +28,10 @@ if [ -n "$EXTRA" ]; then
   # both share cuda:0, gloo gather
   run bench_rehearsal2 600 python bench.py --gpus 2 --steps 5 --warmup 1 --shard-gib 1 --dist-backend gloo --no-cpu-baseline || exit $?
 fi
+if [ -n "$ASAN" ]; then
+  # host-side ASan + UBSan of the C-ABI's host pipelines (make -C examples asan first)
+  run asan_host 600 bash scripts/asan_host.sh || exit $?
+fi
 if [ -n "$PROFILE" ]; then
   B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B || exit $?
