@@ -366,24 +366,46 @@ class Index:
 
     # -- the hot path (src/index.rs:610-659)
     def index_file(self, path, name) -> None:
-        """Cut a file into blocks and add them to the index."""
+        """Cut a file into blocks and add them to the index.
+
+        With a FixedChunker the rows and blocks_hash come from one native
+        pipeline call; the blocks_hash it returns is SHA-1 over the digests in
+        offset order, which is the order the rows are inserted in and so the
+        order compute_blocks_hash's SELECT reads them back in
+        (src/index.rs:661-682) -- the same value without re-reading the rows."""
         with open(path, "rb") as f:  # File::open first: same error on a missing file
             file_id, up_to_date = self.add_file(name, _mtime(f))
             if up_to_date:
                 return
-            if isinstance(self.chunker, FixedChunker):
-                if _seekable(f):
-                    rows_np, _ = host.index_file(path, self.chunker.block_size)
-                else:  # a FIFO: read sequentially from this open, as File::open + read do
-                    rows_np, _ = host.index_fd(f.fileno(), self.chunker.block_size)
-                rows = host.rows_to_tuples(rows_np)
-            else:
+            if not isinstance(self.chunker, FixedChunker):
                 rows = signatures_of_bytes(f.read(), self.chunker)
-        for o, s, d in rows:
-            log.debug("Adding block, offset=%d, size=%d, sha1=%s", o, s, d.hex())
+            elif _seekable(f):
+                rows_np, bh = host.index_file(path, self.chunker.block_size)
+            else:  # a FIFO: read sequentially from this open, as File::open + read do
+                rows_np, bh = host.index_fd(f.fileno(), self.chunker.block_size)
+        if isinstance(self.chunker, FixedChunker):
+            self._insert_rows(file_id, rows_np)
+            self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.hex(), file_id))
+            return
+        if log.isEnabledFor(logging.DEBUG):
+            for o, s, d in rows:
+                log.debug("Adding block, offset=%d, size=%d, sha1=%s", o, s, d.hex())
         self.add_blocks(file_id, rows)
         bh = self.compute_blocks_hash(file_id)
         self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
+
+    def _insert_rows(self, file_id: int, rows, a: int = 0, b: Optional[int] = None) -> None:
+        """add_block for rows[a:b] of a native signature table: the hash column
+        hex-encoded once (HashDigest ToSql, src/lib.rs:78-90), one executemany."""
+        self.begin()
+        b = rows.shape[0] if b is None else b
+        hx = rows["sha1"][a:b].tobytes().hex()
+        offs, sizes = rows["offset"][a:b].tolist(), rows["size"][a:b].tolist()
+        if log.isEnabledFor(logging.DEBUG):
+            for i in range(b - a):
+                log.debug("Adding block, offset=%d, size=%d, sha1=%s", offs[i], sizes[i], hx[40 * i:40 * i + 40])
+        self.db.executemany("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);",
+                            ((hx[40 * i:40 * i + 40], file_id, offs[i], sizes[i]) for i in range(b - a)))
 
     def index_path(self, path, batch_bytes: int = 256 << 20) -> None:
         """Index files and directories recursively (src/index.rs:685-715).
@@ -431,25 +453,18 @@ class Index:
                 if not up_to_date and not _seekable(f):
                     # a FIFO in the tree: read it from this open (a second
                     # open would wait for another writer); rows like index_file
-                    rows = host.rows_to_tuples(host.index_fd(f.fileno(), bs)[0])
-                    self.add_blocks(file_id, rows)
-                    bh = self.compute_blocks_hash(file_id)
-                    self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
+                    rows_np, bh = host.index_fd(f.fileno(), bs)
+                    self._insert_rows(file_id, rows_np)
+                    self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.hex(), file_id))
                     continue
             if not up_to_date:
                 pending.append((file_id, p))
         if not pending:
             return
         rows, first, fh = host.index_files([p for _f, p in pending], bs, stage_bytes=batch_bytes)
-        # Columns converted once for all files (hex = HashDigest ToSql,
-        # src/lib.rs:78-90), then one executemany per file.
-        hx = rows["sha1"].tobytes().hex()
-        offs, sizes = rows["offset"].tolist(), rows["size"].tolist()
         fhx = fh.tobytes().hex()
-        ins = "INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);"
         for k, (file_id, _p) in enumerate(pending):
-            a, b = int(first[k]), int(first[k + 1])
-            self.db.executemany(ins, ((hx[40 * i:40 * i + 40], file_id, offs[i], sizes[i]) for i in range(a, b)))
+            self._insert_rows(file_id, rows, int(first[k]), int(first[k + 1]))
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
 
     def remove_missing_files(self, path) -> None:

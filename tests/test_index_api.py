@@ -169,6 +169,16 @@ def test_index_path_fixed_blocks(gpu, tmp_path, batch_bytes):
     idx.index_path(root, batch_bytes=batch_bytes)
     idx.commit()
     assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
+    # new content: old rows deleted, new rows and blocks_hash stored; the
+    # stored value is still what the reference's SELECT recomputation gives
+    data = oracle.splitmix_bytes(9000, 77)
+    (root / "a.bin").write_bytes(data.tobytes())
+    os.utime(root / "a.bin", ns=(2, 2))
+    idx.index_path(root, batch_bytes=batch_bytes)
+    idx.commit()
+    fid, _, bh = idx.get_file("a.bin")
+    assert bh.bytes == oracle.blocks_hash(oracle.index_fixed(data, 4096)[2])
+    assert idx.compute_blocks_hash(fid) == bh and len(idx.list_file_blocks(fid)) == 3
     os.remove(root / "sub" / "b.bin")
     idx.remove_missing_files(root)
     idx.commit()
