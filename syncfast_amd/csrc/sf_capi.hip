@@ -266,7 +266,7 @@ int sf_index_device_blocks_weak(const void* d_data, uint64_t len, const uint64_t
   return launch_table(d_data, len, d_offsets, d_sizes, n_blocks, d_digests, d_status, as_stream(stream), d_weak);
 }
 
-int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,
+static int sf_index_device_batch_body(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,
                           uint32_t block_size, void* d_digests, uint64_t cap_blocks, void* d_file_hashes,
                           uint64_t* first_block, uint64_t* n_blocks, int* d_status, void* stream) {
   int rc = check_fixed_args(len, block_size);
@@ -439,6 +439,17 @@ int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t s
   hipLaunchKernelGGL(sf::fill_splitmix_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
                      static_cast<uint8_t*>(d_out), len, seed, start);
   return hip_err(hipGetLastError());
+}
+
+}  // extern "C"
+
+// C-ABI entry points: the bodies above, exceptions turned into error codes.
+extern "C" {
+
+int sf_index_device_batch(const void* d_data, uint64_t len, const sf_file_desc* files, uint32_t n_files,
+                          uint32_t block_size, void* d_digests, uint64_t cap_blocks, void* d_file_hashes,
+                          uint64_t* first_block, uint64_t* n_blocks, int* d_status, void* stream) {
+  return guarded([&] { return sf_index_device_batch_body(d_data, len, files, n_files, block_size, d_digests, cap_blocks, d_file_hashes, first_block, n_blocks, d_status, stream); });
 }
 
 }  // extern "C"

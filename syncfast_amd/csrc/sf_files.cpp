@@ -94,7 +94,7 @@ void map_stage(const char* const* paths, const FileStage& st, const std::vector<
 }
 
 // Fill `dst` with the stage's files: (file, <=16 MiB slice) work items taken
-// by up to 8 threads from an atomic counter.
+// by up to io_threads() threads from an atomic counter.
 int read_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, uint8_t* dst,
                std::atomic<int64_t>& bad, const std::vector<const uint8_t*>& mapped) {
   constexpr uint64_t kSlice = 16ull << 20;
@@ -129,10 +129,7 @@ int read_stage(const char* const* paths, const FileStage& st, const std::vector<
   };
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const unsigned nthreads = (unsigned)std::min<size_t>(std::min(io_threads(), hw), std::max<size_t>(1, items.size()));
-  std::vector<std::thread> pool;
-  for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
-  worker();
-  for (auto& th : pool) th.join();
+  run_pool(nthreads, worker);
   return rc.load();
 }
 
@@ -140,7 +137,7 @@ int read_stage(const char* const* paths, const FileStage& st, const std::vector<
 
 extern "C" {
 
-int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes_hint,
+static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes_hint,
                    sf_block_sig* out, uint64_t cap, uint64_t* first_row, uint8_t* blocks_hashes, uint64_t* n_out,
                    uint32_t* bad_file) {
   int rc = check_fixed_args(0, block_size);
@@ -175,10 +172,7 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
     };
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const unsigned nthreads = (unsigned)std::min<uint64_t>(std::min(io_threads(), hw), nchunks);
-    std::vector<std::thread> pool;
-    for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
-    worker();
-    for (auto& th : pool) th.join();
+    run_pool(nthreads, worker);
   }
   uint64_t total = 0;
   for (uint32_t f = 0; f < n_files; f++) {
@@ -283,6 +277,12 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
   std::atomic<int64_t> bad{-1};
   StageMaps maps[2];
   std::vector<const uint8_t*> mptr;
+  struct SyncOnExit {  // destroyed before maps: no mapping is released under an in-flight copy
+    hipStream_t* s;
+    ~SyncOnExit() {
+      for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(s[i]);
+    }
+  } sync_on_exit{streams};
   for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const FileStage& st = stages[k];
@@ -337,6 +337,17 @@ int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_si
       rc = harvest(k);
   if (rc == SF_EIO && bad.load() >= 0) return fail((uint32_t)bad.load(), rc);
   return rc;
+}
+
+}  // extern "C"
+
+// C-ABI entry points: the bodies above, exceptions turned into error codes.
+extern "C" {
+
+int sf_index_files(const char* const* paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes_hint,
+                   sf_block_sig* out, uint64_t cap, uint64_t* first_row, uint8_t* blocks_hashes, uint64_t* n_out,
+                   uint32_t* bad_file) {
+  return guarded([&] { return sf_index_files_body(paths, n_files, block_size, stage_bytes_hint, out, cap, first_row, blocks_hashes, n_out, bad_file); });
 }
 
 }  // extern "C"

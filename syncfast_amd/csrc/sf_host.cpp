@@ -282,7 +282,7 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
 
 extern "C" {
 
-int sf_release_host_cache(void) {
+static int sf_release_host_cache_body(void) {
   for (int d = 0; d < kMaxDevices; d++) {
     std::lock_guard<std::mutex> lk(g_res_mu[d]);  // waits for a call using the set
     if (g_res[d]) {
@@ -299,7 +299,7 @@ int sf_release_host_cache(void) {
 #endif
 static constexpr uint64_t kWireChunk = SF_WIRE_CHUNK_DEFAULT;  // messages per chunk (~9.4 MB at 4 KiB blocks)
 
-int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
+static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
                            uint64_t* n_written, void* stream) {
   if (n_written) *n_written = 0;
   if (block_size == 0 || block_size > SF_MAX_BLOCK_SIZE) return SF_EINVAL;
@@ -539,15 +539,16 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
       return SF_OK;
     };
     const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
-    std::vector<std::thread> pool;
-    std::vector<int> rcs(nthreads, SF_OK);
-    for (unsigned t = 1; t < nthreads && t * slice < n; t++)
-      pool.emplace_back([&, t] { rcs[t] = read_slice(t * slice, std::min(n, (t + 1) * slice)); });
-    rcs[0] = read_slice(0, std::min(n, slice));
-    for (auto& th : pool) th.join();
-    for (int r : rcs)
-      if (r) return r;
-    return SF_OK;
+    const uint64_t nslices = ceil_div(n, slice);
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> rc{SF_OK};
+    run_pool((unsigned)std::min<uint64_t>(nthreads, nslices), [&] {
+      for (uint64_t i; (i = next.fetch_add(1)) < nslices && rc.load() == SF_OK;) {
+        const int r = read_slice(i * slice, std::min(n, (i + 1) * slice));
+        if (r != SF_OK) rc.store(r);
+      }
+    });
+    return rc.load();
   };
   auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
     write_rows(out + first, base / bs + first, nb, dg, bytes, bs);
@@ -560,7 +561,7 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
 
 extern "C" {
 
-int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
+static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
   int rc = check_fixed_args(len, block_size);
   if (rc) return rc;
@@ -578,7 +579,7 @@ int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_b
   });
 }
 
-int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
+static int sf_index_file_body(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
                   uint8_t blocks_hash[20]) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
@@ -650,7 +651,7 @@ int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint
   return rc;
 }
 
-int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t block_size, sf_block_sig* out,
+static int sf_index_file_range_body(const char* path, uint64_t start, uint64_t len, uint32_t block_size, sf_block_sig* out,
                         uint64_t cap, uint64_t* n_out) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
@@ -669,7 +670,7 @@ int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t
   return rc;
 }
 
-int sf_index_fd(int fd, uint32_t block_size, sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[20]) {
+static int sf_index_fd_body(int fd, uint32_t block_size, sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[20]) {
   if (rows) *rows = nullptr;
   if (n_out) *n_out = 0;
   int rc = check_fixed_args(0, block_size);
@@ -697,13 +698,58 @@ int sf_blocks_hash(const uint8_t* digests, uint64_t n, uint8_t out[20]) {
   return SF_OK;
 }
 
-int sf_blocks_hash_sigs(const sf_block_sig* sigs, uint64_t n, uint8_t out[20]) {
+static int sf_blocks_hash_sigs_body(const sf_block_sig* sigs, uint64_t n, uint8_t out[20]) {
   if (!out || (n && !sigs)) return SF_EINVAL;
-  // Gather the digests into one contiguous run (AoS rows are 32 B apart).
-  std::vector<uint8_t> buf(n * 20);
-  for (uint64_t i = 0; i < n; i++) memcpy(buf.data() + 20 * i, sigs[i].sha1, 20);
-  sf_host_sha1_impl(buf.data(), n * 20, out, 0);
+  // The digests gathered into contiguous runs (AoS rows are 32 B apart), a
+  // fixed buffer at a time, streamed through one SHA-1.
+  uint8_t buf[20 * 3276];
+  sf_host_sha1_stream h;
+  sf_host_sha1_begin(&h);
+  for (uint64_t i = 0; i < n;) {
+    const uint64_t m = std::min<uint64_t>(n - i, sizeof(buf) / 20);
+    for (uint64_t j = 0; j < m; j++) memcpy(buf + 20 * j, sigs[i + j].sha1, 20);
+    sf_host_sha1_update(&h, buf, m * 20);
+    i += m;
+  }
+  sf_host_sha1_final(&h, out);
   return SF_OK;
+}
+
+}  // extern "C"
+
+// C-ABI entry points: the bodies above, exceptions turned into error codes.
+extern "C" {
+
+int sf_release_host_cache(void) {
+  return guarded([&] { return sf_release_host_cache_body(); });
+}
+
+int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,
+                           uint64_t* n_written, void* stream) {
+  return guarded([&] { return sf_wire_file_blocks_fd_body(d_digests, n_blocks, block_size, file_len, fd, n_written, stream); });
+}
+
+int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
+                    uint64_t* n_out) {
+  return guarded([&] { return sf_index_buffer_body(data, len, block_size, out, cap, n_out); });
+}
+
+int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
+                  uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_file_body(path, block_size, out, cap, n_out, blocks_hash); });
+}
+
+int sf_index_file_range(const char* path, uint64_t start, uint64_t len, uint32_t block_size, sf_block_sig* out,
+                        uint64_t cap, uint64_t* n_out) {
+  return guarded([&] { return sf_index_file_range_body(path, start, len, block_size, out, cap, n_out); });
+}
+
+int sf_index_fd(int fd, uint32_t block_size, sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_fd_body(fd, block_size, rows, n_out, blocks_hash); });
+}
+
+int sf_blocks_hash_sigs(const sf_block_sig* sigs, uint64_t n, uint8_t out[20]) {
+  return guarded([&] { return sf_blocks_hash_sigs_body(sigs, n, out); });
 }
 
 }  // extern "C"

@@ -18,6 +18,9 @@
 
 #include <algorithm>
 #include <mutex>
+#include <new>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "../../include/syncfast_amd.h"
@@ -33,6 +36,40 @@
   } while (0)
 
 namespace sfi __attribute__((visibility("hidden"))) {
+
+// A C++ exception must not cross the extern "C" boundary: a C or Rust caller
+// would get std::terminate.  Every entry point that allocates, starts threads
+// or takes locks on the host runs its body through guarded(): host allocation
+// failure -> SF_ENOMEM, a thread or lock the system refuses (EAGAIN and the
+// like) -> SF_ENOMEM, anything else -> SF_EIO.
+template <typename F>
+inline int guarded(F&& body) noexcept {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    return SF_ENOMEM;
+  } catch (const std::system_error&) {
+    return SF_ENOMEM;
+  } catch (...) {
+    return SF_EIO;
+  }
+}
+
+// Runs `worker` on the calling thread and on up to nthreads-1 more.  The
+// workers share an atomic work counter, so a thread the system refuses only
+// lowers the parallelism; every started thread is joined before returning
+// (a joinable std::thread destroyed during unwinding would terminate).
+template <typename F>
+inline void run_pool(unsigned nthreads, F&& worker) {
+  std::vector<std::thread> pool;
+  try {
+    pool.reserve(nthreads);
+    for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
+  } catch (...) {
+  }
+  worker();
+  for (auto& th : pool) th.join();
+}
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
