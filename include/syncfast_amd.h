@@ -150,7 +150,9 @@ typedef struct sf_chain_job {
  * (file-major rows) and, in the same launch, up to two chain jobs of EARLIER
  * batches (digests and states written by earlier launches on the same
  * stream), so their blocks_hash latency hides behind this batch's blocks.
- * n_files = 0 runs only the jobs. */
+ * n_files = 0 runs only the jobs.  A batch of more than 2^31 blocks is
+ * SF_EINVAL (one launch per batch; the other entry points split such inputs
+ * into several launches themselves). */
 int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t file_len,
                                   uint32_t block_size, void *d_digests, const sf_chain_job *jobs,
                                   uint32_t n_jobs, void *stream);

@@ -33,6 +33,19 @@ inline int variant_choice() {
 }
 #endif
 
+// Most blocks one launch takes.  HIP caps a launch at 2^32 - 1 work-items
+// (gridDim.x * blockDim.x), i.e. about 2^32 blocks at one lane per block;
+// larger tables -- reachable only with tiny blocks, e.g. 16-B blocks over
+// 64 GiB -- are hashed as several launches over consecutive block ranges
+// (blocks are independent).  A multiple of 16, so every piece of a 16-B
+// aligned fixed tiling stays 16-B aligned.  SF_LAUNCH_MAX_BLOCKS lowers it
+// (test knob: exercises the split at small sizes).
+inline uint64_t launch_max_blocks() {
+  const char* e = getenv("SF_LAUNCH_MAX_BLOCKS");
+  const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  return v ? std::max<uint64_t>(16, v & ~15ull) : (1ull << 31);
+}
+
 inline unsigned grid_for_blocks(uint64_t nblocks) {
   const uint64_t waves = ceil_div(nblocks, 64);
   return (unsigned)ceil_div(waves, sf::kWavesPerWG);
@@ -62,6 +75,17 @@ sf::PadSchedule pad_schedule(uint32_t bytes) {
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
                  hipStream_t stream, uint32_t* weak) {
   if (nblocks == 0) return SF_OK;
+  const uint64_t maxb = launch_max_blocks();
+  if (nblocks > maxb) {  // consecutive pieces of the tiling, one launch each
+    for (uint64_t first = 0; first < nblocks; first += maxb) {
+      const uint64_t cnt = std::min(maxb, nblocks - first), off = first * (uint64_t)bs;
+      const int rc = launch_fixed(static_cast<const uint8_t*>(d_data) + off, std::min(len - off, cnt * (uint64_t)bs),
+                                  bs, cnt, static_cast<uint8_t*>(d_digests) + first * 20, stream,
+                                  weak ? weak + first : nullptr);
+      if (rc) return rc;
+    }
+    return SF_OK;
+  }
   const unsigned grid = grid_for_blocks(nblocks);
   const sf::PadSchedule pad = pad_schedule(bs);
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
@@ -101,6 +125,16 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
                  uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr) {
   if (nblocks == 0) return SF_OK;
+  const uint64_t maxb = launch_max_blocks();
+  if (nblocks > maxb) {  // consecutive pieces of the table, one launch each
+    for (uint64_t first = 0; first < nblocks; first += maxb) {
+      const int rc = launch_table(d_data, len, d_offsets + first, d_sizes + first, std::min(maxb, nblocks - first),
+                                  static_cast<uint8_t*>(d_digests) + first * 20, d_status, stream,
+                                  weak ? weak + first : nullptr);
+      if (rc) return rc;
+    }
+    return SF_OK;
+  }
   const unsigned grid = grid_for_blocks(nblocks);
   if (weak)
     hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, true>), dim3(grid), dim3(sf::kThreads), 0, stream,
@@ -157,7 +191,7 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
       S = cand;
       break;
     }
-  if (!d_status || ceil_div(nfiles, 64 * sf::kWavesPerWG) > device_cus()) S = 1;
+  if (!d_status || ceil_div(nfiles, 64 * sf::kWavesPerWG) > device_cus() || nbf * nfiles > launch_max_blocks()) S = 1;
   if (S == 1) {
     int rc = launch_fixed(base, nbf * nfiles * (uint64_t)bs, bs, nbf * nfiles, dig, s);
     if (rc) return rc;
@@ -189,8 +223,23 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   return rc;
 }
 
+// The FILE_BLOCK messages of digests [0, n): every message is 33 + digits(bs)
+// bytes but the last, whose size field is `last`.
 int launch_wire(const uint8_t* d_digests, uint64_t n, uint32_t bs, uint32_t last, uint8_t* d_out,
                 hipStream_t stream) {
+  if (n == 0) return SF_OK;
+  const uint64_t maxb = launch_max_blocks();
+  if (n > maxb) {  // consecutive runs of messages, one launch each
+    uint64_t db = 1;
+    for (uint64_t v = bs; v >= 10; v /= 10) db++;
+    for (uint64_t first = 0; first < n; first += maxb) {
+      const uint64_t cnt = std::min(maxb, n - first);
+      const int rc = launch_wire(d_digests + first * 20, cnt, bs, first + cnt == n ? last : bs,
+                                 d_out + first * (33 + db), stream);
+      if (rc) return rc;
+    }
+    return SF_OK;
+  }
   hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, d_digests,
                      n, bs, last, d_out);
   return hip_err(hipGetLastError());
@@ -379,6 +428,7 @@ int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t
   if (n_jobs > 2 || (n_jobs && !jobs)) return SF_EINVAL;
   const uint64_t total = n_files ? (file_len / block_size) * n_files : 0;
   if (total && (!d_data || !d_digests)) return SF_EINVAL;
+  if (total > launch_max_blocks()) return SF_EINVAL;  // one launch per batch: split the batch
   sf::ChainJob cj[2] = {};
   for (uint32_t k = 0; k < n_jobs; k++) {
     const sf_chain_job& j = jobs[k];
@@ -426,9 +476,8 @@ int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_
   if (bytes > cap) return SF_ENOSPC;
   if (!nb) return SF_OK;
   if (!d_digests || !d_out) return SF_EINVAL;
-  hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(nb, 256)), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint8_t*>(d_digests), nb, block_size, last, static_cast<uint8_t*>(d_out));
-  return hip_err(hipGetLastError());
+  return launch_wire(static_cast<const uint8_t*>(d_digests), nb, block_size, last, static_cast<uint8_t*>(d_out),
+                     as_stream(stream));
 }
 
 int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t start, void* stream) {
