@@ -60,58 +60,6 @@ inline uint64_t stage_bytes(uint32_t bs) {
   return nb * bs;
 }
 
-// Shared driver of sf_index_buffer / sf_index_file: `read(dst, off, n)`
-// fills a pinned staging buffer with input bytes [off, off+n).
-template <typename ReadFn>
-int index_pipelined(uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap, uint64_t* n_out, ReadFn read) {
-  const uint64_t nblocks = len ? ceil_div(len, bs) : 0;
-  if (n_out) *n_out = nblocks;
-  if (nblocks > cap) return SF_ENOSPC;
-  if (nblocks == 0) return SF_OK;
-  const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
-  const uint64_t nstages = ceil_div(len, stage);
-  HostLease res;
-  hipStream_t* st;
-  hipEvent_t* done;
-  void *ddata[2], *pin[2], *ddig, *pdig;
-  int rc = res.streams(st, done);
-  for (int i = 0; i < 2 && rc == SF_OK; i++) {
-    rc = res.dev(i, stage, &ddata[i]);
-    if (rc == SF_OK) rc = res.pin(i, stage, &pin[i]);
-  }
-  if (rc == SF_OK) rc = res.dev(2, nblocks * 20, &ddig);
-  if (rc == SF_OK) rc = res.pin(2, nblocks * 20, &pdig);
-  if (rc != SF_OK) return rc;
-  for (uint64_t k = 0; k < nstages && rc == SF_OK; k++) {
-    const int b = (int)(k & 1);
-    const uint64_t off = k * stage;
-    const uint64_t n = std::min(stage, len - off);
-    if (k >= 2) {
-      if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
-    }
-    rc = read(static_cast<uint8_t*>(pin[b]), off, n);
-    if (rc != SF_OK) break;
-    if (hipMemcpyAsync(ddata[b], pin[b], n, hipMemcpyHostToDevice, st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
-    const uint64_t first_blk = off / bs;
-    const uint64_t nb = ceil_div(n, bs);
-    rc = launch_fixed(ddata[b], n, bs, nb, static_cast<uint8_t*>(ddig) + first_blk * 20, st[b]);
-    if (rc != SF_OK) break;
-    if (hipEventRecord(done[b], st[b]) != hipSuccess) { rc = SF_ENODEV; break; }
-  }
-  for (int i = 0; i < 2; i++)
-    if (hipStreamSynchronize(st[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
-  if (rc != SF_OK) return rc;
-  SF_HIP(hipMemcpyAsync(pdig, ddig, nblocks * 20, hipMemcpyDeviceToHost, st[0]));
-  SF_HIP(hipStreamSynchronize(st[0]));
-  const uint8_t* dg = static_cast<const uint8_t*>(pdig);
-  for (uint64_t i = 0; i < nblocks; i++) {
-    out[i].offset = i * bs;
-    out[i].size = (uint32_t)std::min<uint64_t>(bs, len - i * bs);
-    memcpy(out[i].sha1, dg + 20 * i, 20);
-  }
-  return SF_OK;
-}
-
 // In-place route of sf_index_buffer / sf_index_file: the DMA engine reads the
 // caller's pages (or the page-cache pages of a mapped file) directly, no
 // staging memcpy.  Per ~256 MiB stage, on alternating streams: H2D, the
@@ -375,8 +323,8 @@ static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks,
 
 namespace {
 
-// Staged file pipeline (sf_index_file's pread route and the sequential
-// route of sf_index_fd): two pinned stages of whole blocks (the last one
+// Staged pipeline (sf_index_file's pread route, the sequential route of
+// sf_index_fd, sf_index_buffer below its in-place size): two pinned stages of whole blocks (the last one
 // short).  `fill(dst, off, cap, &n, &eof)` puts the next input bytes into a
 // pinned stage; per stage, on alternating streams, H2D + block kernel + D2H of
 // the stage's digests.  While stage k is being filled, stage k-1 is on the
@@ -573,10 +521,22 @@ static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t bloc
     rc = index_inplace(data, len, block_size, out, cap, n_out, nullptr);
     if (rc != SF_ENOTSUP) return rc;
   }
-  return index_pipelined(len, block_size, out, cap, n_out, [&](uint8_t* dst, uint64_t off, uint64_t n) {
-    memcpy(dst, data + off, n);
+  // Staged: memcpy into the pinned stages, the file route's pipeline.
+  const uint64_t nb = len ? ceil_div(len, block_size) : 0;
+  if (n_out) *n_out = nb;
+  if (nb > cap) return SF_ENOSPC;
+  if (nb == 0) return SF_OK;
+  auto fill = [&](uint8_t* dst, uint64_t off, uint64_t scap, uint64_t* n, bool* eof) {
+    *n = std::min(scap, len - off);
+    *eof = off + *n >= len;
+    memcpy(dst, data + off, *n);
     return SF_OK;
-  });
+  };
+  auto emit = [&](uint64_t first, uint64_t nbk, const uint8_t* dg, uint64_t bytes) {
+    write_rows(out + first, first, nbk, dg, bytes, block_size);
+    return SF_OK;
+  };
+  return staged_pipeline(block_size, std::min(file_stage_bytes(block_size), nb * block_size), fill, emit, nullptr);
 }
 
 static int sf_index_file_body(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,
