@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import stat
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -46,8 +47,18 @@ def release_cache() -> None:
 def index_file(path, block_size: int) -> Tuple[np.ndarray, bytes]:
     """Signatures of a file on disk + its blocks_hash.  A regular file that
     grows between the sizing stat and the call (SF_ENOSPC with the new need)
-    is indexed again with room for it, as index_files does."""
-    size = os.path.getsize(path)
+    is indexed again with room for it, as index_files does.  Anything else
+    that opens (a FIFO, a character device) is read to EOF through index_fd:
+    sized by a stat, its bytes would be consumed by a call whose rows did
+    not fit."""
+    st = os.stat(path)
+    if not stat.S_ISREG(st.st_mode):
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            return index_fd(fd, block_size)
+        finally:
+            os.close(fd)
+    size = st.st_size
     n = (size + block_size - 1) // block_size if size else 0
     nout = ctypes.c_uint64(0)
     bh = (ctypes.c_uint8 * 20)()

@@ -91,6 +91,18 @@ def test_sf_index_file_on_fifo_reports_need(gpu, tmp_path):
     assert rc == SF_ENOSPC and nout.value == 10
 
 
+def test_host_index_file_on_fifo(gpu, tmp_path):
+    # host.index_file on a FIFO: read once to EOF (a stat says 0 bytes; a
+    # sized call would consume the stream and then ask for room)
+    fifo = tmp_path / "fifo3"
+    os.mkfifo(fifo)
+    data = oracle.splitmix_bytes(7 * 4096 + 3, 714)
+    th = _writer(fifo, data.tobytes())
+    rows, bh = host.index_file(fifo, 4096)
+    th.join(timeout=60)
+    _check(rows, bh, data, 4096)
+
+
 def test_index_fd_regular_file_from_offset(gpu, tmp_path):
     # a regular file's descriptor is read from its current position
     p = tmp_path / "f"
