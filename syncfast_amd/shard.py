@@ -91,19 +91,39 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
     and computes its blocks_hash (src/index.rs:661-682 chains over every
     digest, so it runs once, after the gather).
 
+    The file's length is `dst`'s stat of it, broadcast, so every rank cuts the
+    same shards even if the file changes meanwhile.  Before the gather the
+    ranks agree on success: a rank whose read fails (the file shrank under
+    it, an I/O error) raises its SfError and every other rank raises too,
+    instead of waiting in a gather that rank never joins.
+
     Returns (rows SIG_DTYPE[n], blocks_hash bytes) on `dst`, None elsewhere.
-    `device`: where the gather's tensors live (the rank's GPU for RCCL; None
-    = host tensors, for gloo)."""
+    `device`: where the collectives' tensors live (the rank's GPU for RCCL;
+    None = host tensors, for gloo).  `dst` is a rank of the default group."""
     import os
 
     import numpy as np
 
     from . import host
+    from ._lib import SF_EIO, SfError
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    size = os.path.getsize(path)
+    where = device if device is not None else torch.device("cpu")
+    size_t = torch.tensor([os.path.getsize(path) if rank == dst else 0], dtype=torch.int64, device=where)
+    dist.broadcast(size_t, src=dst, group=group)
+    size = int(size_t.item())
     start, ln = shard_range(size, block_size, world, rank)
-    rows = host.index_file_range(path, start, ln, block_size)
+    failure: Optional[BaseException] = None
+    try:
+        rows = host.index_file_range(path, start, ln, block_size)
+    except (SfError, OSError) as e:
+        failure = e
+    failed = torch.tensor([1 if failure is not None else 0], dtype=torch.int32, device=where)
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=group)
+    if failure is not None:
+        raise failure
+    if int(failed.item()):
+        raise SfError(SF_EIO, f"index_file_sharded: another rank failed to index its shard of {os.fsdecode(path)}")
     dig = torch.from_numpy(np.ascontiguousarray(rows["sha1"]).reshape(-1, 20))
     if device is not None:
         dig = dig.to(device)

@@ -125,3 +125,43 @@ def test_index_file_sharded_rebuilds_rows(tmp_path, world, total, bs):
     assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
     assert np.array_equal(rows["sha1"], want)
     assert bh == oracle.blocks_hash(want)
+
+
+def _failing_worker(rank, world, port, path, bs, q):
+    import syncfast_amd.host as h
+    from syncfast_amd._lib import SF_EIO, SfError
+    from syncfast_amd.shard import index_file_sharded
+
+    def fake(path, start, length, bs_):
+        if rank == world - 1:  # this rank's read fails (e.g. the file shrank under it)
+            raise SfError(SF_EIO, "sf_index_file_range")
+        return _fake_index_file_range(path, start, length, bs_)
+    h.index_file_range = fake
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        index_file_sharded(path, bs)
+        q.put((rank, "returned"))
+    except SfError as e:
+        q.put((rank, "SfError" if e.code == SF_EIO else f"code {e.code}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_index_file_sharded_one_rank_fails_all_raise(tmp_path):
+    # no rank is left waiting in the gather: every rank raises
+    p = tmp_path / "f"
+    oracle.splitmix_bytes(4096 * 10, 1).tofile(p)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, str(p), 4096, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert got == {r: "SfError" for r in range(world)}
