@@ -14,6 +14,7 @@ Reference mapping (/root/reference):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Optional, Sequence, Tuple
 
@@ -29,11 +30,13 @@ __all__ = [
 ]
 
 
-def _require_device(t: torch.Tensor, name: str, dtype=None) -> None:
+def _require_device(t: torch.Tensor, name: str, dtype=None, device: Optional[torch.device] = None) -> None:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if t.device.type != "cuda":
         raise ValueError(f"{name} must be on a ROCm device (got {t.device}); syncfast_amd has no CPU path")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, the input on {device}")
     if dtype is not None and t.dtype != dtype:
         raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
     if not t.is_contiguous():
@@ -43,6 +46,20 @@ def _require_device(t: torch.Tensor, name: str, dtype=None) -> None:
 def _stream_ptr(t: torch.Tensor, stream: Optional[torch.cuda.Stream]) -> int:
     s = stream if stream is not None else torch.cuda.current_stream(t.device)
     return s.cuda_stream
+
+
+@contextlib.contextmanager
+def _on(device: torch.device, stream: Optional[torch.cuda.Stream]):
+    """`device` current and, if given, `stream` its current stream: outputs
+    and status words are then allocated, zeroed and read back on the stream
+    the kernel runs on (a status word zeroed or read on another stream races
+    with the kernel that writes it)."""
+    with torch.cuda.device(device):
+        if stream is None:
+            yield
+        else:
+            with torch.cuda.stream(stream):
+                yield
 
 
 def num_blocks(length: int, block_size: int) -> int:
@@ -55,19 +72,28 @@ def index_device(data: torch.Tensor, block_size: int, out: Optional[torch.Tensor
     """SHA-1 of every fixed-size block of a uint8 HBM buffer -> uint8[n, 20]."""
     _require_device(data, "data", torch.uint8)
     n = num_blocks(data.numel(), block_size)
-    if out is None:
-        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
-    else:
-        _require_device(out, "out", torch.uint8)
-        if out.numel() < 20 * n:
-            raise ValueError(f"out holds {out.numel() // 20} digests, need {n}")
-    nb = ctypes.c_uint64(0)
-    with torch.cuda.device(data.device):
+    with _on(data.device, stream):
+        if out is None:
+            out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+        else:
+            _require_device(out, "out", torch.uint8, data.device)
+            if out.numel() < 20 * n:
+                raise ValueError(f"out holds {out.numel() // 20} digests, need {n}")
+        nb = ctypes.c_uint64(0)
         check(lib().sf_index_device_fixed(data.data_ptr() if data.numel() else None, data.numel(),
                                           block_size, out.data_ptr() if n else None, out.numel() // 20,
                                           ctypes.byref(nb), _stream_ptr(data, stream)),
               "sf_index_device_fixed")
     return out
+
+
+def _blocks_args(data, offsets, sizes):
+    _require_device(data, "data", torch.uint8)
+    _require_device(offsets, "offsets", torch.int64, data.device)
+    _require_device(sizes, "sizes", torch.int32, data.device)
+    if sizes.numel() != offsets.numel():
+        raise ValueError("offsets and sizes differ in length")
+    return offsets.numel()
 
 
 def index_device_blocks(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
@@ -78,27 +104,24 @@ def index_device_blocks(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.
     ``offsets`` int64 and ``sizes`` int32 tensors on the same device.  With
     ``check_range`` a block outside the buffer raises SfError(SF_ERANGE)
     (this synchronises the stream)."""
-    _require_device(data, "data", torch.uint8)
-    _require_device(offsets, "offsets", torch.int64)
-    _require_device(sizes, "sizes", torch.int32)
-    n = offsets.numel()
-    if sizes.numel() != n:
-        raise ValueError("offsets and sizes differ in length")
-    if out is None:
-        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
-    elif out.numel() < 20 * n:
-        raise ValueError("out too small")
-    if n == 0:
-        return out
-    status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
-    with torch.cuda.device(data.device):
+    n = _blocks_args(data, offsets, sizes)
+    with _on(data.device, stream):
+        if out is None:
+            out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+        else:
+            _require_device(out, "out", torch.uint8, data.device)
+            if out.numel() < 20 * n:
+                raise ValueError("out too small")
+        if n == 0:
+            return out
+        status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
         check(lib().sf_index_device_blocks(data.data_ptr() if data.numel() else None, data.numel(),
                                            offsets.data_ptr(), sizes.data_ptr(), n, out.data_ptr(),
                                            status.data_ptr() if status is not None else None,
                                            _stream_ptr(data, stream)),
               "sf_index_device_blocks")
-    if status is not None and int(status.item()) != 0:
-        raise SfError(SF_ERANGE, "sf_index_device_blocks")
+        if status is not None and int(status.item()) != 0:
+            raise SfError(SF_ERANGE, "sf_index_device_blocks")
     return out
 
 
@@ -110,16 +133,16 @@ def index_device_weak(data: torch.Tensor, block_size: int, out: Optional[torch.T
     (SURVEY.md 8a row a8)."""
     _require_device(data, "data", torch.uint8)
     n = num_blocks(data.numel(), block_size)
-    if out is None:
-        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
-    if weak_out is None:
-        weak_out = torch.empty(n, dtype=torch.int32, device=data.device)
-    _require_device(out, "out", torch.uint8)
-    _require_device(weak_out, "weak_out", torch.int32)
-    if out.numel() < 20 * n or weak_out.numel() < n:
-        raise ValueError(f"outputs too small for {n} blocks")
-    nb = ctypes.c_uint64(0)
-    with torch.cuda.device(data.device):
+    with _on(data.device, stream):
+        if out is None:
+            out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+        if weak_out is None:
+            weak_out = torch.empty(n, dtype=torch.int32, device=data.device)
+        _require_device(out, "out", torch.uint8, data.device)
+        _require_device(weak_out, "weak_out", torch.int32, data.device)
+        if out.numel() < 20 * n or weak_out.numel() < n:
+            raise ValueError(f"outputs too small for {n} blocks")
+        nb = ctypes.c_uint64(0)
         check(lib().sf_index_device_fixed_weak(data.data_ptr() if data.numel() else None, data.numel(), block_size,
                                                out.data_ptr() if n else None, weak_out.data_ptr() if n else None,
                                                min(out.numel() // 20, weak_out.numel()), ctypes.byref(nb),
@@ -132,25 +155,20 @@ def index_device_blocks_weak(data: torch.Tensor, offsets: torch.Tensor, sizes: t
                              check_range: bool = True, stream: Optional[torch.cuda.Stream] = None):
     """index_device_blocks plus the opt-in Adler-32 per block (0 for a block
     outside the buffer) -> (digests uint8[n, 20], weak int32[n])."""
-    _require_device(data, "data", torch.uint8)
-    _require_device(offsets, "offsets", torch.int64)
-    _require_device(sizes, "sizes", torch.int32)
-    n = offsets.numel()
-    if sizes.numel() != n:
-        raise ValueError("offsets and sizes differ in length")
-    out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
-    weak = torch.empty(n, dtype=torch.int32, device=data.device)
-    if n == 0:
-        return out, weak
-    status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
-    with torch.cuda.device(data.device):
+    n = _blocks_args(data, offsets, sizes)
+    with _on(data.device, stream):
+        out = torch.empty((n, 20), dtype=torch.uint8, device=data.device)
+        weak = torch.empty(n, dtype=torch.int32, device=data.device)
+        if n == 0:
+            return out, weak
+        status = torch.zeros(1, dtype=torch.int32, device=data.device) if check_range else None
         check(lib().sf_index_device_blocks_weak(data.data_ptr() if data.numel() else None, data.numel(),
                                                 offsets.data_ptr(), sizes.data_ptr(), n, out.data_ptr(),
                                                 weak.data_ptr(), status.data_ptr() if status is not None else None,
                                                 _stream_ptr(data, stream)),
               "sf_index_device_blocks_weak")
-    if status is not None and int(status.item()) != 0:
-        raise SfError(SF_ERANGE, "sf_index_device_blocks_weak")
+        if status is not None and int(status.item()) != 0:
+            raise SfError(SF_ERANGE, "sf_index_device_blocks_weak")
     return out, weak
 
 
@@ -175,24 +193,28 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
     for i, (o, ln) in enumerate(files):
         descs[i].offset, descs[i].len = int(o), int(ln)
         total += num_blocks(int(ln), block_size)
-    if out is None:
-        out = torch.empty((total, 20), dtype=torch.uint8, device=data.device)
-    elif out.numel() < 20 * total:
-        raise ValueError("out too small")
-    dig = out
-    fh = None
-    if file_hashes and nf:
-        fh = hashes_out if hashes_out is not None else torch.empty((nf, 20), dtype=torch.uint8, device=data.device)
-        if fh.numel() < 20 * nf:
-            raise ValueError("hashes_out too small")
-    first = np.zeros(nf + 1, np.uint64)
-    nb = ctypes.c_uint64(0)
-    own_status = status is None and fh is not None
-    if own_status:
-        status = torch.zeros(1, dtype=torch.int32, device=data.device)
-    elif status is not None:
-        _require_device(status, "status", torch.int32)
-    with torch.cuda.device(data.device):
+    with _on(data.device, stream):
+        if out is None:
+            out = torch.empty((total, 20), dtype=torch.uint8, device=data.device)
+        else:
+            _require_device(out, "out", torch.uint8, data.device)
+            if out.numel() < 20 * total:
+                raise ValueError("out too small")
+        dig = out
+        fh = None
+        if file_hashes and nf:
+            if hashes_out is not None:
+                _require_device(hashes_out, "hashes_out", torch.uint8, data.device)
+            fh = hashes_out if hashes_out is not None else torch.empty((nf, 20), dtype=torch.uint8, device=data.device)
+            if fh.numel() < 20 * nf:
+                raise ValueError("hashes_out too small")
+        first = np.zeros(nf + 1, np.uint64)
+        nb = ctypes.c_uint64(0)
+        own_status = status is None and fh is not None
+        if own_status:
+            status = torch.zeros(1, dtype=torch.int32, device=data.device)
+        elif status is not None:
+            _require_device(status, "status", torch.int32, data.device)
         check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs, nf,
                                           block_size, dig.data_ptr() if total else None, dig.numel() // 20,
                                           fh.data_ptr() if fh is not None else None,
@@ -200,10 +222,10 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
                                           status.data_ptr() if status is not None else None,
                                           _stream_ptr(data, stream)),
               "sf_index_device_batch")
-    if own_status:
-        code = int(status.item())
-        if code != 0:
-            raise SfError(code, "sf_index_device_batch")
+        if own_status:
+            code = int(status.item())
+            if code != 0:
+                raise SfError(code, "sf_index_device_batch")
     return dig, first.astype(np.int64), fh
 
 
@@ -274,7 +296,7 @@ class BatchStream:
 
     def push(self, data: torch.Tensor, digests: torch.Tensor):
         _require_device(data, "data", torch.uint8)
-        _require_device(digests, "digests", torch.uint8)
+        _require_device(digests, "digests", torch.uint8, data.device)
         if data.numel() != self.n_files * self.file_len or digests.numel() < 20 * self.n_files * self.nbf:
             raise ValueError("batch or digest table has the wrong size")
         jobs, done = self._step_jobs()

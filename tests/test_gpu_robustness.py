@@ -199,3 +199,22 @@ def test_concurrent_mixed_host_calls(gpu, tmp_path):
 
     with cf.ThreadPoolExecutor(7) as ex:
         assert sorted(ex.map(job, range(7))) == list(range(7))
+
+
+def test_side_stream_status_is_read_on_that_stream(gpu):
+    # status words are zeroed, written and read on the caller's stream: an
+    # out-of-range block on a side stream, queued behind a long kernel there,
+    # is still reported; a clean call on the same stream is not
+    data = torch.from_numpy(oracle.splitmix_bytes(1 << 20, 3)).to(gpu)
+    big = torch.empty(1 << 30, dtype=torch.uint8, device=gpu)
+    s = torch.cuda.Stream(device=gpu)
+    offs = torch.tensor([0, 1 << 20], dtype=torch.int64, device=gpu)
+    sizes = torch.tensor([100, 1], dtype=torch.int32, device=gpu)
+    for _ in range(3):
+        device.index_device(big, 4096, stream=s)  # keeps the side stream busy
+        with pytest.raises(SfError):
+            device.index_device_blocks(data, offs, sizes, stream=s)
+        device.index_device(big, 4096, stream=s)
+        got = device.index_device_blocks(data, offs[:1], sizes[:1], stream=s)
+        s.synchronize()
+        assert bytes(got[0].cpu().numpy()) == oracle.sha1(oracle.splitmix_bytes(100, 3))
