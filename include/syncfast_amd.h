@@ -43,7 +43,7 @@ extern "C" {
 
 #define SF_OK 0
 #define SF_EIO (-5)      /* file read failed */
-#define SF_ENOMEM (-12)  /* device / pinned allocation failed */
+#define SF_ENOMEM (-12)  /* device, pinned or host allocation failed, or the system refused a thread */
 #define SF_ENODEV (-19)  /* no HIP device, or a HIP runtime error */
 #define SF_EINVAL (-22)  /* bad argument */
 #define SF_ENOSPC (-28)  /* output capacity too small; *n_out holds the need */
