@@ -207,7 +207,18 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     const uint4* my = wave_tile + lane * PIECES;
     const uint8_t* span_ptr = data + geo.base;
 
-#if SF_SCALAR_ISSUE
+#if defined(SF_EXPERIMENT_SEQ)
+    // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_SEQ, 4 KiB
+    // blocks): the same DMA volume per step, but one contiguous 64*TILE-byte
+    // piece of the wave's span instead of TILE bytes of each of 64 blocks
+    // 4 KiB apart (wrong digests) -- isolates the cost of the strided pattern.
+#define SF_ISSUE(step)                                                                     \
+  do {                                                                                     \
+    uint32_t vs[PIECES];                                                                   \
+    for (int j = 0; j < PIECES; ++j) vs[j] = (step) * (uint32_t)TILE * 63u + j * 1024u + lane * 16u; \
+    issue_step<TILE>(span_ptr, geo.span, (step), vs, wave_tile);                           \
+  } while (0)
+#elif SF_SCALAR_ISSUE
     const uint64_t ptr_s = uniform_u64(reinterpret_cast<uint64_t>(span_ptr));
     const uint64_t span_s = uniform_u64(geo.span);
 #define SF_ISSUE(step) issue_step_s<TILE>(ptr_s, span_s, (step), voff, wave_tile)
