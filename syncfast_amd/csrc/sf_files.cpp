@@ -10,8 +10,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <stdio.h>
+
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -21,6 +24,32 @@
 using namespace sfi;
 
 namespace {
+
+// SF_TRACE=1: phase times of each sf_index_files call on stderr (probe only).
+struct Trace {
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  double stat_ms = 0, big_ms = 0, wait_ms = 0, harvest_ms = 0, read_ms = 0, issue_ms = 0;
+  Trace() {
+    const char* e = getenv("SF_TRACE");
+    on = e && atoi(e);
+    t0 = last = std::chrono::steady_clock::now();
+  }
+  void lap(double& acc) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    acc += std::chrono::duration<double, std::milli>(now - last).count();
+    last = now;
+  }
+  void report(uint32_t files, size_t stages) {
+    if (!on) return;
+    const double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr,
+            "sf_index_files trace: %u files, %zu stages: stat %.2f big %.2f read %.2f issue %.2f wait %.2f "
+            "harvest %.2f total %.2f ms\n",
+            files, stages, stat_ms, big_ms, read_ms, issue_ms, wait_ms, harvest_ms, tot);
+  }
+};
 
 struct FileStage {
   std::vector<uint32_t> files;    // file indices, in order
@@ -144,6 +173,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
   if (rc) return rc;
   if (n_files && (!paths || !first_row || !blocks_hashes)) return SF_EINVAL;
   const uint32_t bs = block_size;
+  Trace tr;
   auto fail = [&](uint32_t f, int code) {
     if (bad_file) *bad_file = f;
     return code;
@@ -174,6 +204,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
     const unsigned nthreads = (unsigned)std::min<uint64_t>(std::min(io_threads(), hw), nchunks);
     run_pool(nthreads, worker);
   }
+  tr.lap(tr.stat_ms);
   uint64_t total = 0;
   for (uint32_t f = 0; f < n_files; f++) {
     if (st_rc[f] != SF_OK) return fail(f, st_rc[f]);
@@ -211,6 +242,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
     if (rc == SF_ENOSPC || (rc == SF_OK && got != want)) return fail(f, SF_EIO);  // changed meanwhile
     if (rc) return rc == SF_EIO ? fail(f, rc) : rc;
   }
+  tr.lap(tr.big_ms);
   if (stages.empty()) return SF_OK;
 
   // 3. Pipeline: read stage k (host threads) while stage k-1 copies and
@@ -286,13 +318,17 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
   for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const FileStage& st = stages[k];
+    tr.lap(tr.issue_ms);
     if (k >= 2) {
       if (hipEventSynchronize(done[b]) != hipSuccess) { rc = SF_ENODEV; break; }
+      tr.lap(tr.wait_ms);
       if ((rc = harvest(k - 2)) != SF_OK) break;
+      tr.lap(tr.harvest_ms);
     }
     maps[b].release();  // stage k-2's copies are done (its event was waited for above)
     map_stage(paths, st, size, maps[b], mptr);
     rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad, mptr);
+    tr.lap(tr.read_ms);
     if (rc) break;
     hipStream_t s = streams[b];
     // H2D: each mapped file from its mapping, every run of consecutive
@@ -329,12 +365,16 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
       break;
     }
   }
+  tr.lap(tr.issue_ms);
   for (int i = 0; i < 2; i++)
     if (hipStreamSynchronize(streams[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
+  tr.lap(tr.wait_ms);
   for (int i = 0; i < 2; i++) maps[i].release();  // every copy has completed
   if (rc == SF_OK)
     for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size() && rc == SF_OK; k++)
       rc = harvest(k);
+  tr.lap(tr.harvest_ms);
+  tr.report(n_files, stages.size());
   if (rc == SF_EIO && bad.load() >= 0) return fail((uint32_t)bad.load(), rc);
   return rc;
 }

@@ -183,6 +183,19 @@ class HostLease {
       *out = slot;
       return SF_OK;
     }
+    // Cached buffers grow in steps (powers of two to 16 MiB, then 16 MiB
+    // multiples): a stage of packed small files (just under 256 MiB) and then
+    // a stage of 8 MiB files (exactly 256 MiB) share one allocation instead of
+    // paying a free + reallocation of every stage buffer (~0.13 ms per MiB,
+    // pinned and device: scripts/files_trace.py, scripts/pin_alloc_probe.py).
+    if (need <= kCacheMax) {
+      uint64_t r = need <= (16ull << 20) ? 4096 : need;
+      if (need <= (16ull << 20))
+        while (r < need) r <<= 1;
+      else
+        r = (need + (16ull << 20) - 1) & ~((16ull << 20) - 1);
+      need = std::min(r, kCacheMax);
+    }
     void* p = nullptr;
     if (pinned) SF_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
     else SF_HIP(hipMalloc(&p, need));
