@@ -6,7 +6,8 @@ coalesced streaming read (16 B/lane loads and buffer_load ... lds alike), so it
 is doubled; WRITE_SIZE is exact for streaming stores.  Averages over every
 launch of the SHA-1 kernel in the pass.  The entry records the SHA-256 of the
 library the passes ran and of its gfx950 code objects (bench.py reports traffic
-only for the same code objects).
+only for the same code objects).  Only the full-shard launches count (the
+largest grid of the pass).
 
 usage: python scripts/pmc_traffic.py FETCH_CSV WRITE_CSV CONFIG_KEY SHARD_BYTES [OUT]
 """
@@ -23,8 +24,12 @@ LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "syncfast_a
 
 
 def avg(path, counter, match="sha1_fixed_kernel"):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if match in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    """Mean counter value over the SHA-1 kernel's launches of the full shard
+    (the largest grid in the pass): the bench's clock-ramp and timed steps,
+    not its smaller end-to-end stage launches."""
+    rows = [r for r in csv.DictReader(open(path)) if match in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    grid = max(int(r["Grid_Size"]) for r in rows)
+    vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == grid]
     return sum(vals) / len(vals), len(vals)
 
 
