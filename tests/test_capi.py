@@ -176,3 +176,32 @@ def test_traffic_profile_is_for_these_kernels():
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
         tr = json.load(f)
     assert tr["config2"]["code_object_sha256"] == h
+
+
+@pytest.mark.parametrize("n", [0, 1, 3276, 3277, 10_000])
+def test_blocks_hash_sigs_across_its_gather_buffer(n):
+    # sf_blocks_hash_sigs gathers digests a fixed buffer (3276 rows) at a time
+    rows = np.zeros(max(n, 1), host.SIG_DTYPE)[:n]
+    rows["sha1"] = np.random.default_rng(n).integers(0, 256, (n, 20), dtype=np.uint8)
+    out = (ctypes.c_uint8 * 20)()
+    assert syncfast_amd.lib().sf_blocks_hash_sigs(rows.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)), n, out) == 0
+    assert bytes(out) == hashlib.sha1(rows["sha1"].tobytes()).digest()
+
+
+def test_pmc_traffic_averages_full_shard_launches(tmp_path):
+    # scripts/pmc_traffic.py: only the largest grid of the pass counts (the
+    # bench's shard launches), not smaller launches in the same process
+    import csv
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_traffic", os.path.join(ROOT, "scripts", "pmc_traffic.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    p = tmp_path / "pmc.csv"
+    with open(p, "w", newline="") as f:
+        w = csv.DictWriter(f, ["Dispatch_Id", "Grid_Size", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for i, (grid, v) in enumerate([(2097152, 100.0), (2097152, 102.0), (65536, 3.0), (16777216, 7.0)]):
+            name = "sf::fill_splitmix_kernel" if grid == 16777216 else "void sf::sha1_fixed_kernel<128, 1, false>"
+            w.writerow({"Dispatch_Id": i, "Grid_Size": grid, "Kernel_Name": name, "Counter_Name": "FETCH_SIZE",
+                        "Counter_Value": v})
+    assert mod.avg(str(p), "FETCH_SIZE") == (101.0, 2)
