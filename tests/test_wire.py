@@ -23,6 +23,57 @@ def test_other_messages():
     assert wire.write_message("FileEnd") + wire.write_message("Complete") == b"FILE_END\nCOMPLETE\n"
 
 
+
+def test_reference_test_parse():
+    # proto::tests::test_parse, src/sync/ssh/proto.rs:483-510: the same byte
+    # pieces, the same messages after each piece
+    inputs = [b"FILE_ENTR", b"Y", b"\n", b"filename\n12", b"\n12345678901234567890\nCOMPLETE", b"\n"]
+    expected = [[], [], [], [], [("FileEntry", b"filename", 12, HashDigest(b"12345678901234567890"))], [("Complete",)]]
+    p = wire.Parser()
+    for piece, want in zip(inputs, expected):
+        assert p.receive(piece) == want
+
+
+def test_parse_round_trips_every_message_bytewise():
+    d = HashDigest(bytes(range(20)))
+    msgs = [("FileEntry", b"dir/f", 123456789, d), ("EndFiles",), ("GetFile", b"dir/f"), ("FileStart", b"x"),
+            ("FileBlock", d, 4096), ("FileBlock", HashDigest(b"\n" * 20), 7), ("FileEnd",), ("GetBlock", d),
+            ("BlockData", d, b"a\nb\n"), ("BlockData", d, b""), ("Complete",)]
+    stream = b"".join(wire.write_message(*m) for m in msgs)
+    p = wire.Parser()
+    got = []
+    for i in range(len(stream)):  # one byte at a time: every split point
+        got += p.receive(stream[i:i + 1])
+    assert got == msgs
+    assert wire.Parser().receive(stream) == msgs
+
+
+@pytest.mark.parametrize("data,err", [
+    (b"X" * 20, "Unterminated command"),
+    (b"NOPE\n", "Unknown command"),
+    (b"GET_FILE\n" + b"f" * 100, "Unterminated filename"),
+    (b"FILE_BLOCK\n" + b"d" * 20 + b"x", "Unterminated digest"),
+    (b"FILE_BLOCK\n" + b"d" * 20 + b"\n-1\n", "Invalid block size"),
+    (b"FILE_BLOCK\n" + b"d" * 20 + b"\n1 \n", "Invalid block size"),
+    (b"FILE_BLOCK\n" + b"d" * 20 + b"\n" + b"1" * 15, "Unterminated size"),
+    (b"FILE_ENTRY\nf\n1a\n", "Invalid file size"),
+    (b"FILE_ENTRY\nf\n" + b"1" * 16 + b"\n", "Unterminated size"),
+    (b"BLOCK_DATA\n" + b"d" * 20 + b"\n2\nabc", "Invalid data end byte"),
+])
+def test_parse_errors(data, err):
+    with pytest.raises(wire.ProtocolError, match=err):
+        wire.Parser().receive(data)
+
+
+def test_parse_limits_and_usize_forms():
+    # a line of exactly its limit is accepted; Rust's usize::from_str takes a leading '+'
+    p = wire.Parser()
+    assert p.receive(b"GET_FILE\n" + b"f" * 100 + b"\n") == [("GetFile", b"f" * 100)]
+    d = b"d" * 20
+    assert p.receive(b"FILE_BLOCK\n" + d + b"\n+12\n") == [("FileBlock", HashDigest(d), 12)]
+    assert p.receive(b"FILE_BLOCK\n" + d + b"\n" + b"9" * 15 + b"\n") == [("FileBlock", HashDigest(d), 10 ** 15 - 1)]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bs", [(4096 * 10 + 7, 4096), (65536 * 3, 65536), (999, 100), (5, 4096)])
 def test_file_blocks_device_matches_write_message(gpu, n, bs):
@@ -54,3 +105,19 @@ def test_file_blocks_to_fd_streams_the_same_bytes(gpu, tmp_path, monkeypatch, n,
     if n < 10_000:
         _, sizes, want_d = oracle.index_fixed(data, bs)
         assert want == b"".join(wire.write_message("FileBlock", bytes(dd), int(sz)) for dd, sz in zip(want_d, sizes))
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bs", [(4096 * 2500 + 7, 4096), (999, 100), (65536 * 8, 65536)])
+def test_device_run_parses_back_to_the_rows(gpu, n, bs):
+    # a destination's parser over the device-built FILE_BLOCK run gets the
+    # file's rows back: every digest and every block size, in order
+    data = oracle.splitmix_bytes(n, n + 2)
+    dig = device.index_device(torch.from_numpy(data.copy()).to(gpu), bs)
+    run = wire.file_blocks_device(dig, bs, n).cpu().numpy().tobytes()
+    msgs = wire.Parser().receive(run)
+    _, sizes, want = oracle.index_fixed(data, bs)
+    assert [m[0] for m in msgs] == ["FileBlock"] * len(want)
+    assert [m[1].bytes for m in msgs] == [bytes(w) for w in want]
+    assert [m[2] for m in msgs] == [int(x) for x in sizes]
