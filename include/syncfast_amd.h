@@ -157,6 +157,27 @@ int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t
                                   uint32_t block_size, void *d_digests, const sf_chain_job *jobs,
                                   uint32_t n_jobs, void *stream);
 
+/* ------------------------------------ the receiving side of a sync ---- */
+
+/* Block lookup of a sync destination.  For every FILE_BLOCK of an incoming
+ * file, FsDestinationInner::sink (src/sync/fs.rs:461-476) asks its index
+ * whether it holds that block: Index::get_block (src/index.rs:77-103), the
+ * first row with that hash and present = 1, SQLite's (hash, rowid) index
+ * order.  A block set is that question for a whole table at once: built on
+ * the device from the destination's rows -- d_table, n_rows x 20-B digests in
+ * rowid order (4-B aligned; the caller keeps it alive while the set is used),
+ * d_present, one byte per row (non-zero = present; NULL = all present) --
+ * then sf_block_set_lookup writes, for each of n_query digests at d_query,
+ * the index of the first present row with that digest, or -1, to d_rows
+ * (device int64).  Asynchronous on `stream`; n_rows <= 2^31.
+ * sf_block_set_free releases the set (stream-ordered). */
+typedef struct sf_block_set sf_block_set;
+int sf_block_set_build(const void *d_table, const uint8_t *d_present, uint64_t n_rows,
+                       sf_block_set **out, void *stream);
+int sf_block_set_lookup(const sf_block_set *set, const void *d_query, uint64_t n_query,
+                        int64_t *d_rows, void *stream);
+int sf_block_set_free(sf_block_set *set, void *stream);
+
 /* The signature table as the reference's wire messages, on the device:
  * n_blocks FILE_BLOCK messages, "FILE_BLOCK\n" + 20 digest bytes + "\n" +
  * decimal block size + "\n" (write_message, src/sync/ssh/proto.rs:162-166),

@@ -180,6 +180,33 @@ def adler_blocks(data, offsets, sizes) -> np.ndarray:
     return out
 
 
+def block_lookup(table, present, queries) -> np.ndarray:
+    """Index::get_block (src/index.rs:77-103) for many digests at once: for
+    each query the first row (rowid order) whose digest equals it and whose
+    present flag is set, or -1 -- the row SQLite returns first from
+    idx_blocks_hash, (hash, rowid) order.  ``table`` uint8[n, 20] in rowid
+    order, ``present`` bool[n] or None (all present), ``queries`` uint8[m, 20].
+    Sort-based (numpy), so it handles millions of rows."""
+    t = np.ascontiguousarray(np.asarray(table, np.uint8).reshape(-1, 20))
+    q = np.ascontiguousarray(np.asarray(queries, np.uint8).reshape(-1, 20))
+    rows = np.arange(t.shape[0], dtype=np.int64)
+    if present is not None:
+        keep = np.asarray(present).astype(bool).reshape(-1)
+        t, rows = t[keep], rows[keep]
+    out = np.full(q.shape[0], -1, np.int64)
+    if t.shape[0] == 0 or q.shape[0] == 0:
+        return out
+    key = np.dtype((np.void, 20))
+    tk = t.view(key).reshape(-1)
+    uniq, first = np.unique(tk, return_index=True)  # first occurrence = smallest row among kept rows
+    qk = q.view(key).reshape(-1)
+    pos = np.searchsorted(uniq, qk)
+    pos_c = np.minimum(pos, uniq.shape[0] - 1)
+    hit = (pos < uniq.shape[0]) & (uniq[pos_c] == qk)
+    out[hit] = rows[first[pos_c[hit]]]
+    return out
+
+
 def splitmix_bytes(length: int, seed: int, start: int = 0) -> np.ndarray:
     out = np.empty(length, np.uint8)
     lib().sfo_fill_splitmix(_ptr(out), length, seed & MASK64, start)

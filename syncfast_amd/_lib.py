@@ -33,6 +33,7 @@ EXPORTED = (
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
+    "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
 
 
@@ -93,6 +94,9 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_blocks_hash.argtypes = [vp, u64, vp]
     L.sf_blocks_hash_sigs.argtypes = [ctypes.POINTER(BlockSig), u64, vp]
     L.sf_sha1_host.argtypes = [vp, u64, vp]
+    L.sf_block_set_build.argtypes = [vp, vp, u64, ctypes.POINTER(vp), vp]
+    L.sf_block_set_lookup.argtypes = [vp, vp, u64, vp, vp]
+    L.sf_block_set_free.argtypes = [vp, vp]
     for name in EXPORTED:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int
@@ -125,11 +129,13 @@ def check(rc: int, what: str = "") -> None:
         raise SfError(rc, what)
 
 
-def code_object_sha256(path: str = None) -> str:
-    """SHA-256 of the gfx950 code objects inside the library (its
-    ``.hip_fatbin`` section): what the GPU runs.  Host-only changes to the
-    library leave it unchanged; any kernel change alters it.  bench.py keys
-    the PMC traffic of profiles/traffic.json on it."""
+def code_object_sha256(path: str = None, kernel: bytes = b"sha1_fixed_kernel") -> str:
+    """SHA-256 of the gfx950 code object that holds `kernel` (the library's
+    ``.hip_fatbin`` section holds one clang offload bundle per GPU translation
+    unit; the SHA-1 kernels are in sf_capi.hip's).  What the GPU runs for that
+    kernel: host-only changes, and changes to other translation units' kernels,
+    leave it unchanged; any change to the SHA-1 kernels alters it.  bench.py
+    keys the PMC traffic of profiles/traffic.json on it."""
     import hashlib
     import struct
     with open(path or LIB_PATH, "rb") as f:
@@ -140,11 +146,27 @@ def code_object_sha256(path: str = None) -> str:
     shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
     secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
     stro = secs[shstrndx][4]
+    fat = None
     for sec in secs:
         name = b[stro + sec[0]: b.index(b"\0", stro + sec[0])]
         if name == b".hip_fatbin":
-            return hashlib.sha256(b[sec[4]: sec[4] + sec[5]]).hexdigest()
-    raise ValueError("no .hip_fatbin section")
+            fat = b[sec[4]: sec[4] + sec[5]]
+    if fat is None:
+        raise ValueError("no .hip_fatbin section")
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos = fat.find(magic)
+    while pos >= 0:  # bundle: magic, u64 entries, then (u64 offset, u64 size, u64 triple length, triple)
+        n, = struct.unpack_from("<Q", fat, pos + len(magic))
+        p = pos + len(magic) + 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fat, p)
+            triple = fat[p + 24: p + 24 + tlen]
+            p += 24 + tlen
+            co = fat[pos + off: pos + off + size]
+            if triple.startswith(b"hipv4-amdgcn") and kernel in co:
+                return hashlib.sha256(co).hexdigest()
+        pos = fat.find(magic, pos + 1)
+    raise ValueError(f"no code object holds {kernel!r}")
 
 
 def device_count() -> int:

@@ -26,7 +26,7 @@ from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
 __all__ = [
     "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
     "index_device_weak", "index_device_blocks_weak", "BatchStream",
-    "fill_splitmix", "splitmix_tensor",
+    "fill_splitmix", "splitmix_tensor", "BlockSet",
 ]
 
 
@@ -313,6 +313,71 @@ class BatchStream:
             if done is not None:
                 out.append(done)
         return out
+
+
+class BlockSet:
+    """The receiving side's block lookup, on the device (sf_block_set_*).
+
+    Built from a destination index's rows -- ``table`` uint8[n, 20] digests
+    in rowid order, ``present`` bool/uint8[n] (None = all present) -- as an
+    HBM hash table; ``lookup(digests)`` returns int64[m]: for each digest the
+    row of the first present row holding it, or -1.  That is Index::get_block
+    (src/index.rs:77-103: hash = ? AND present = 1, SQLite's (hash, rowid)
+    order) for a whole FILE_BLOCK list at once, the question
+    FsDestinationInner::sink asks per message (src/sync/fs.rs:461-476).
+    The set reads ``table`` at lookup time: keep it unchanged while in use."""
+
+    def __init__(self, table: torch.Tensor, present: Optional[torch.Tensor] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
+        _require_device(table, "table", torch.uint8)
+        if table.dim() != 2 or table.shape[1] != 20:
+            raise ValueError("table must be uint8[n, 20]")
+        n = table.shape[0]
+        if present is not None:
+            if present.dtype == torch.bool:
+                present = present.view(torch.uint8)
+            _require_device(present, "present", torch.uint8, table.device)
+            if present.numel() != n:
+                raise ValueError("present must hold one flag per row")
+        self.table, self.present, self.stream = table, present, stream
+        self._h = ctypes.c_void_p()
+        with _on(table.device, stream):
+            check(lib().sf_block_set_build(table.data_ptr() if n else None,
+                                           present.data_ptr() if present is not None and n else None, n,
+                                           ctypes.byref(self._h), _stream_ptr(table, stream)),
+                  "sf_block_set_build")
+
+    def lookup(self, digests: torch.Tensor) -> torch.Tensor:
+        _require_device(digests, "digests", torch.uint8, self.table.device)
+        if digests.dim() != 2 or digests.shape[1] != 20:
+            raise ValueError("digests must be uint8[m, 20]")
+        if not self._h:
+            raise ValueError("BlockSet is closed")
+        m = digests.shape[0]
+        with _on(self.table.device, self.stream):
+            rows = torch.empty(m, dtype=torch.int64, device=self.table.device)
+            if m:
+                check(lib().sf_block_set_lookup(self._h, digests.data_ptr(), m, rows.data_ptr(),
+                                                _stream_ptr(self.table, self.stream)), "sf_block_set_lookup")
+        return rows
+
+    def close(self) -> None:
+        if self._h:
+            with _on(self.table.device, self.stream):
+                check(lib().sf_block_set_free(self._h, _stream_ptr(self.table, self.stream)), "sf_block_set_free")
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def fill_splitmix(out: torch.Tensor, seed: int, start: int = 0,

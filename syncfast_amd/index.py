@@ -223,6 +223,31 @@ class Index:
             "WHERE blocks.hash = ? AND blocks.present = 1;", (hash.to_sql(),)).fetchone()
         return (PurePath(row[0]), int(row[1]), int(row[2])) if row else None
 
+    def get_blocks(self, hashes: Sequence[HashDigest], device=None) -> List[Optional[Tuple[PurePath, int, int]]]:
+        """get_block for a whole list of hashes -- a FILE_BLOCK run as the
+        destination receives it (src/sync/fs.rs:461-476) -- answered by one
+        device lookup (syncfast_amd.device.BlockSet, sf_block_set_*): the
+        index's rows in rowid order go to the GPU as a hash table, and each
+        hash gets the row get_block would return (present, joined to a file,
+        first in rowid order), or None."""
+        import torch
+
+        from .device import BlockSet
+        rows = self.db.execute(
+            "SELECT blocks.hash, blocks.present = 1 AND files.file_id IS NOT NULL, files.name, blocks.offset, "
+            "blocks.size FROM blocks LEFT JOIN files ON blocks.file_id = files.file_id "
+            "ORDER BY blocks.rowid;").fetchall()
+        if not hashes:
+            return []
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        table = np.frombuffer(bytes.fromhex("".join(r[0] for r in rows)), np.uint8).reshape(-1, 20)
+        present = np.fromiter((bool(r[1]) for r in rows), bool, len(rows))
+        q = np.frombuffer(b"".join(h.bytes for h in hashes), np.uint8).reshape(-1, 20)
+        t = torch.from_numpy(table.copy()).to(dev)
+        with BlockSet(t, torch.from_numpy(present).to(dev)) as bset:
+            found = bset.lookup(torch.from_numpy(q.copy()).to(dev)).cpu().numpy()
+        return [None if r < 0 else (PurePath(rows[r][2]), int(rows[r][3]), int(rows[r][4])) for r in found]
+
     def get_file(self, name) -> Optional[Tuple[int, DateTimeUtc, Optional[HashDigest]]]:
         row = self.db.execute(
             "SELECT file_id, modified, blocks_hash FROM files WHERE name = ? AND temporary = 0;",
