@@ -13,7 +13,8 @@
  *   ./sf_index [-b block_size] [-m | -B | -s N] path...
  *     -m: all paths through one sf_index_files call; -B: each file from a host
  *     buffer (sf_index_buffer); -s N: each file as N sf_index_file_range shards;
- *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout
+ *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
+ *     -L dst src: src's blocks looked up among dst's (sf_block_set_*)
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -142,6 +143,60 @@ static int wire_synthetic(uint64_t n, uint32_t bs) {
     return rc;
 }
 
+/* -L: the receiving side's lookup from C.  dst's rows are the destination's
+ * index (digests in row order, all present); src's rows are the FILE_BLOCK
+ * run it receives.  Each src block is looked up in a device block set built
+ * from dst's digests (sf_block_set_*), as FsDestinationInner::sink asks
+ * Index::get_block per block (src/sync/fs.rs:461-476): "i row" per src block,
+ * row = dst row holding that digest first, or -1. */
+static int lookup_blocks(const char *dst, const char *src, uint32_t bs) {
+    sf_block_sig *rows[2] = {NULL, NULL};
+    uint64_t n[2] = {0, 0};
+    const char *paths[2] = {dst, src};
+    uint8_t bh[20];
+    int rc = SF_OK;
+    for (int k = 0; k < 2 && rc == SF_OK; k++) {
+        struct stat sb;
+        if (stat(paths[k], &sb) != 0 || !S_ISREG(sb.st_mode)) { rc = SF_EIO; break; }
+        const uint64_t cap = sb.st_size ? ((uint64_t)sb.st_size + bs - 1) / bs : 0;
+        rows[k] = malloc((cap ? cap : 1) * sizeof(sf_block_sig));
+        rc = rows[k] ? sf_index_file(paths[k], bs, rows[k], cap, &n[k], bh) : SF_ENOMEM;
+    }
+    uint8_t *h_dig[2] = {NULL, NULL};
+    void *d_dig[2] = {NULL, NULL};
+    int64_t *h_rows = NULL, *d_rows = NULL;
+    sf_block_set *set = NULL;
+    for (int k = 0; k < 2 && rc == SF_OK; k++) {  /* digests, 20 B apart, to the device */
+        h_dig[k] = malloc(n[k] ? n[k] * 20 : 20);
+        if (!h_dig[k]) { rc = SF_ENOMEM; break; }
+        for (uint64_t i = 0; i < n[k]; i++) memcpy(h_dig[k] + 20 * i, rows[k][i].sha1, 20);
+        if (hipMalloc(&d_dig[k], n[k] ? n[k] * 20 : 20) != hipSuccess ||
+            hipMemcpy(d_dig[k], h_dig[k], n[k] * 20, hipMemcpyHostToDevice) != hipSuccess)
+            rc = SF_ENOMEM;
+    }
+    if (rc == SF_OK) {
+        h_rows = malloc((n[1] ? n[1] : 1) * sizeof(int64_t));
+        rc = (h_rows && hipMalloc((void **)&d_rows, (n[1] ? n[1] : 1) * sizeof(int64_t)) == hipSuccess) ? SF_OK
+                                                                                                       : SF_ENOMEM;
+    }
+    if (rc == SF_OK) rc = sf_block_set_build(d_dig[0], NULL, n[0], &set, NULL);
+    if (rc == SF_OK) rc = sf_block_set_lookup(set, d_dig[1], n[1], d_rows, NULL);
+    if (rc == SF_OK && hipMemcpy(h_rows, d_rows, n[1] * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = SF_ENODEV;
+    if (rc == SF_OK)
+        for (uint64_t i = 0; i < n[1]; i++) printf("%llu %lld\n", (unsigned long long)i, (long long)h_rows[i]);
+    if (set) sf_block_set_free(set, NULL);
+    (void)hipDeviceSynchronize();
+    for (int k = 0; k < 2; k++) {
+        if (d_dig[k]) (void)hipFree(d_dig[k]);
+        free(h_dig[k]);
+        free(rows[k]);
+    }
+    if (d_rows) (void)hipFree(d_rows);
+    free(h_rows);
+    return rc;
+}
+
 /* -m: every path through ONE sf_index_files call (index_path's pipeline,
  * src/index.rs:685-715), rows sized by a first call with cap 0. */
 static int index_many(char **paths, int n, uint32_t bs) {
@@ -169,7 +224,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0, buffer = 0, shards = 0;
+    int many = 0, buffer = 0, shards = 0, lookup = 0;
     long long wire = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -177,11 +232,13 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-s") == 0) shards = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-w") == 0) wire = atoll(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
+        else if (strcmp(argv[i], "-L") == 0) lookup = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
         else break;
     }
     if (i >= argc && wire < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path... | -w bytes\n", argv[0]);
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path... | -w bytes | -L dst src\n",
+                argv[0]);
         return 2;
     }
     int ndev = 0;
@@ -197,6 +254,12 @@ int main(int argc, char **argv) {
         return rc != SF_OK;
     }
     int status = 0;
+    if (lookup) {
+        const int rc = i + 2 == argc ? lookup_blocks(argv[i], argv[i + 1], bs) : SF_EINVAL;
+        if (rc != SF_OK) fprintf(stderr, "lookup: %s\n", sf_strerror(rc));
+        sf_release_host_cache();
+        return rc != SF_OK;
+    }
     if (many) {
         status = index_many(argv + i, argc - i, bs) != SF_OK;
         sf_release_host_cache();

@@ -8,6 +8,7 @@ import os
 import subprocess
 import threading
 
+import numpy as np
 import pytest
 
 import oracle
@@ -90,3 +91,24 @@ def test_c_consumer_device_path_and_wire(gpu, n, bs):
     offs, sizes, dig = oracle.index_fixed(oracle.splitmix_bytes(n, 0x5EED0000), bs)
     want = b"".join(wire.write_message("FileBlock", HashDigest(bytes(d)), int(s)) for d, s in zip(dig, sizes))
     assert r.stdout == want
+
+
+@pytest.mark.gpu
+def test_c_consumer_block_lookup(gpu, tmp_path):
+    # -L dst src: src's blocks looked up among dst's rows through
+    # sf_block_set_* from C; the answers equal the oracle's first-row lookup
+    bs = 4096
+    rng = np.random.default_rng(5)
+    a = oracle.splitmix_bytes(300 * bs, 41).reshape(300, bs)
+    a[250:260] = a[10:20]  # repeated blocks inside dst: the first row wins
+    fresh = oracle.splitmix_bytes(50 * bs, 42).reshape(50, bs)
+    b = np.concatenate([a[rng.integers(0, 300, 150)], fresh])
+    rng.shuffle(b)
+    pa, pb = tmp_path / "dst", tmp_path / "src"
+    a.tofile(pa)
+    b.tofile(pb)
+    r = subprocess.run([_built(False), "-L", "-b", str(bs), str(pa), str(pb)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    got = [int(ln.split()[1]) for ln in r.stdout.decode().splitlines()]
+    want = oracle.block_lookup(oracle.index_fixed(a.reshape(-1), bs)[2], None, oracle.index_fixed(b.reshape(-1), bs)[2])
+    assert got == want.tolist() and sum(g >= 0 for g in got) == 150
