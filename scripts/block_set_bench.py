@@ -62,6 +62,28 @@ def main():
     print(f"build: {n} rows in {t_build:.3f} ms ({n / t_build / 1e6:.2f} G rows/s)", flush=True)
     print(f"lookup: {m} digests ({m // 2} hits) in {t_look:.3f} ms = {m / t_look / 1e6:.2f} G lookups/s, "
           f"{alg / t_look / 1e6:.1f} GB/s of algorithmic bytes", flush=True)
+    # beyond the caches: 2^25 rows (640 MiB of digests, 512 MiB of slots),
+    # uniform random digests (SHA-1 output is uniform), 2^25 lookups, half hits
+    big_n = 1 << 25
+    big = torch.randint(0, 256, (big_n, 20), dtype=torch.uint8, device="cuda")
+    bq = torch.cat([big[torch.randint(0, big_n, (big_n // 2,), device="cuda")],
+                    torch.randint(0, 256, (big_n // 2, 20), dtype=torch.uint8, device="cuda")])
+    hb = {}
+
+    def build_big():
+        if "s" in hb:
+            hb["s"].close()
+        hb["s"] = BlockSet(big)
+    tb = events(build_big, 3)
+    tl = events(lambda: hb["s"].lookup(bq), 5)
+    algb = big_n * (20 + 8 + 8) + (big_n // 2) * 20
+    print(f"2^25-row table: build {tb:.2f} ms ({big_n / tb / 1e6:.2f} G rows/s), 2^25 lookups {tl:.2f} ms = "
+          f"{big_n / tl / 1e6:.2f} G lookups/s, {algb / tl / 1e6:.1f} GB/s of algorithmic bytes", flush=True)
+    gb = hb["s"].lookup(bq)  # property check: hits find their own digest, fresh digests miss
+    half = big_n // 2
+    assert bool((gb[:half] >= 0).all()) and torch.equal(big[gb[:half]], bq[:half]) and bool((gb[half:] == -1).all())
+    hb["s"].close()
+    del big, bq
     # numpy oracle (sort-based), the same question on the host cores
     tq = q.cpu().numpy()
     tt = dig.cpu().numpy()
