@@ -462,8 +462,11 @@ class Index:
         else:
             if rel.parts[:1] == (".",):
                 rel = PurePath(*rel.parts[1:])
+            # index_path on a file: the reference's rel is Path::new(""), whose
+            # name is the empty string (PurePath("") would print as ".")
+            name = "" if rel == PurePath("") else rel
             log.info("Indexing file %s (%s)", rel, p)
-            todo.append((p, rel))
+            todo.append((p, name))
 
     def _index_batched(self, todo, batch_bytes: int) -> None:
         """Every file needing (re)indexing through ONE native pipeline

@@ -279,3 +279,15 @@ def test_mtime_gate_at_nanosecond_resolution(gpu, tmp_path):
     bh2 = idx.get_file("f")[2]
     want = oracle.index_fixed(oracle.splitmix_bytes(50_000, 2), 4096)[2]
     assert bh2.bytes == oracle.blocks_hash(want) != bh1.bytes
+
+
+def test_walk_of_a_file_names_it_empty(tmp_path):
+    # index_path(file): rel = Path::new("") (src/index.rs:686, 706-713), so the
+    # file is indexed under the empty name, not "."
+    p = tmp_path / "single"
+    p.write_bytes(b"x")
+    todo = []
+    Index.open_in_memory()._index_path_rec(p, PurePath(""), todo)
+    assert len(todo) == 1 and todo[0][1] == ""
+    from syncfast_amd.index import _name_str
+    assert _name_str(todo[0][1]) == ""
