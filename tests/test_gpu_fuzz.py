@@ -158,3 +158,23 @@ def test_fuzz_index_files(gpu, case, tmp_path):
         if want.shape[0]:
             assert np.array_equal(r["sha1"], want) and np.array_equal(r["offset"], offs)
         assert bytes(fh[k]) == oracle.blocks_hash(want)
+
+
+@pytest.mark.parametrize("case", range(40))
+def test_fuzz_block_set(gpu, case):
+    # destination tables drawn from a small digest pool (many repeats), random
+    # present flags; queries from the pool and fresh: vs the first-row oracle
+    from syncfast_amd.device import BlockSet
+    rng = np.random.default_rng(15_000 + case)
+    pool = rng.integers(0, 256, (int(rng.integers(1, 400)), 20), dtype=np.uint8)
+    if rng.integers(0, 2):  # pool digests that share slot bits and fingerprint
+        pool[:, :11] = pool[0, :11]
+    n = int(rng.integers(0, 5000))
+    table = pool[rng.integers(0, pool.shape[0], n)] if n else np.zeros((0, 20), np.uint8)
+    present = rng.random(n) < rng.random() if rng.integers(0, 2) else None
+    q = np.concatenate([pool, rng.integers(0, 256, (int(rng.integers(0, 50)), 20), dtype=np.uint8)])
+    t = torch.from_numpy(np.ascontiguousarray(table)).to(gpu)
+    pres = torch.from_numpy(present).to(gpu) if present is not None else None
+    with BlockSet(t, pres) as bset:
+        got = bset.lookup(torch.from_numpy(q).to(gpu)).cpu().numpy()
+    assert np.array_equal(got, oracle.block_lookup(table, present, q)), (n, pool.shape[0])
