@@ -169,8 +169,10 @@ int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t
  * d_present, one byte per row (non-zero = present; NULL = all present) --
  * then sf_block_set_lookup writes, for each of n_query digests at d_query,
  * the index of the first present row with that digest, or -1, to d_rows
- * (device int64).  Asynchronous on `stream`; n_rows <= 2^31.
- * sf_block_set_free releases the set (stream-ordered). */
+ * (device int64).  Asynchronous on `stream`; n_rows <= 2^31.  Lookups only
+ * read the set: any number may run at once, on any streams ordered after the
+ * build.  sf_block_set_free releases the set (stream-ordered: after the
+ * lookups on that stream). */
 typedef struct sf_block_set sf_block_set;
 int sf_block_set_build(const void *d_table, const uint8_t *d_present, uint64_t n_rows,
                        sf_block_set **out, void *stream);
