@@ -264,7 +264,7 @@ class BatchStream:
     def _launch(self, data, digests, jobs, ref):
         from ._lib import ChainJob
         arr = (ChainJob * max(len(jobs), 1))(*jobs)
-        with torch.cuda.device(ref.device):
+        with _on(ref.device, self.stream):
             check(lib().sf_index_device_batch_chained(
                 data.data_ptr() if data is not None else None, self.n_files if data is not None else 0,
                 self.file_len, self.block_size, digests.data_ptr() if digests is not None else None,
@@ -299,17 +299,21 @@ class BatchStream:
         _require_device(digests, "digests", torch.uint8, data.device)
         if data.numel() != self.n_files * self.file_len or digests.numel() < 20 * self.n_files * self.nbf:
             raise ValueError("batch or digest table has the wrong size")
-        jobs, done = self._step_jobs()
-        self._launch(data, digests, jobs, data)
-        self._b = (digests, torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device))
+        # the chain states and this batch's blocks_hash table are allocated on
+        # the stream the launches run on, like every other output here
+        with _on(data.device, self.stream):
+            jobs, done = self._step_jobs()
+            self._launch(data, digests, jobs, data)
+            self._b = (digests, torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device))
         return done
 
     def finish(self):
         out = []
         while self._a is not None or self._b is not None:
             ref = (self._a or self._b)[0]
-            jobs, done = self._step_jobs()
-            self._launch(None, None, jobs, ref)
+            with _on(ref.device, self.stream):
+                jobs, done = self._step_jobs()
+                self._launch(None, None, jobs, ref)
             if done is not None:
                 out.append(done)
         return out

@@ -57,7 +57,8 @@ def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
     async_op, returns (work, finish) where finish() -> table after
     work.wait()."""
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    rank = dist.get_rank(group)  # shard index: the rank within `group`
+    is_dst = dist.get_rank() == dst  # `dst` is a global rank, as dist.gather takes it
     counts = shard_blocks(total_len, block_size, world)
     if local.shape[0] != counts[rank]:
         raise ValueError(f"rank {rank} holds {local.shape[0]} digests, shard has {counts[rank]}")
@@ -69,11 +70,11 @@ def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
         padded[:local.shape[0]] = local
     else:
         padded = local
-    bufs = [torch.empty_like(padded) for _ in range(world)] if rank == dst else None
+    bufs = [torch.empty_like(padded) for _ in range(world)] if is_dst else None
     work = dist.gather(padded, bufs, dst=dst, group=group, async_op=async_op)
 
     def finish():
-        if rank != dst:
+        if not is_dst:
             return None
         return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
@@ -107,9 +108,10 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
     from . import host
     from ._lib import SF_EIO, SfError
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    rank = dist.get_rank(group)  # shard index: the rank within `group`
+    is_dst = dist.get_rank() == dst  # `dst` is a global rank, as the collectives take it
     where = device if device is not None else torch.device("cpu")
-    size_t = torch.tensor([os.path.getsize(path) if rank == dst else 0], dtype=torch.int64, device=where)
+    size_t = torch.tensor([os.path.getsize(path) if is_dst else 0], dtype=torch.int64, device=where)
     dist.broadcast(size_t, src=dst, group=group)
     size = int(size_t.item())
     start, ln = shard_range(size, block_size, world, rank)
@@ -128,7 +130,7 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
     if device is not None:
         dig = dig.to(device)
     table = gather_digests(dig, size, block_size, group=group, dst=dst)
-    if rank != dst:
+    if not is_dst:
         return None
     table = table.cpu().numpy()
     n = table.shape[0]

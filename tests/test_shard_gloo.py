@@ -165,3 +165,43 @@ def test_index_file_sharded_one_rank_fails_all_raise(tmp_path):
         pr.join(timeout=120)
         assert pr.exitcode == 0
     assert got == {r: "SfError" for r in range(world)}
+
+
+def _subgroup_worker(rank, world, port, path, bs, q):
+    import syncfast_amd.host as h
+    from syncfast_amd.shard import index_file_sharded
+    h.index_file_range = _fake_index_file_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group([1, 2])  # every rank takes part in new_group
+        if rank in (1, 2):
+            # dst is a GLOBAL rank (2), which is rank 1 inside the subgroup
+            res = index_file_sharded(path, bs, group=sub, dst=2)
+            q.put((rank, None if res is None else (res[0].tobytes(), res[1])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_index_file_sharded_subgroup_global_dst(tmp_path):
+    from syncfast_amd.host import SIG_DTYPE
+    p = tmp_path / "f"
+    total, bs = 4096 * 21 + 7, 4096
+    data = oracle.splitmix_bytes(total, 0x5EED0009)
+    data.tofile(p)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, str(p), bs, q)) for r in range(3)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert got[1] is None
+    rows = np.frombuffer(got[2][0], SIG_DTYPE)
+    offs, sizes, want = oracle.index_fixed(data, bs)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    assert np.array_equal(rows["sha1"], want) and got[2][1] == oracle.blocks_hash(want)
