@@ -15,6 +15,8 @@
 #include <atomic>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "sf_internal.hpp"
 #include "sf_kernels.hpp"
 
@@ -122,10 +124,61 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   return hip_err(hipGetLastError());
 }
 
+// Explicit block lists of at least this many blocks are hashed in order of
+// length (sha1_table_kernel's `order`): a wave runs as long as its longest
+// block, so 64 blocks of mixed sizes side by side waste most lanes -- a list
+// of content-defined sizes (mean 8 KiB, up to 32 KiB) hashed at 312 GiB/s in
+// list order against 1834 GiB/s sorted (scripts/ragged_probe.py).  Below a
+// few waves per wave slot the sort cannot shorten the launch (every wave is
+// resident at once and the longest block sets the time), so small lists keep
+// their order.  SF_TABLE_SORT=0 / 1 never / always sorts (test knob).
+inline uint64_t table_sort_min() {
+  const char* e = getenv("SF_TABLE_SORT");
+  if (e) return atoi(e) ? 1 : ~0ull;
+  return 1ull << 17;
+}
+constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.5 GiB of workspace at most)
+
+// Stream-ordered workspace holding the processing order of blocks [0, n) of
+// a list: stable radix sort of (compression count, index), descending, with
+// rocprim on `s`.  Returns nullptr (unsorted launch) if anything fails.
+uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
+  *ws_out = nullptr;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  uint16_t *kin = nullptr, *kout = nullptr;
+  uint32_t *iin = nullptr, *iout = nullptr;
+  size_t tmp = 0;
+  if (rocprim::radix_sort_pairs_desc(nullptr, tmp, kin, kout, iin, iout, (unsigned)n, 0u, 16u, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp);
+  uint8_t* ws = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  kin = reinterpret_cast<uint16_t*>(ws);
+  kout = reinterpret_cast<uint16_t*>(ws + kb);
+  iin = reinterpret_cast<uint32_t*>(ws + 2 * kb);
+  iout = reinterpret_cast<uint32_t*>(ws + 2 * kb + ib);
+  hipLaunchKernelGGL(sf::table_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, kin, iin);
+  if (hipGetLastError() != hipSuccess ||
+      rocprim::radix_sort_pairs_desc(ws + 2 * kb + 2 * ib, tmp, kin, kout, iin, iout, (unsigned)n, 0u, 16u, s) !=
+          hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFreeAsync(ws, s);
+    return nullptr;
+  }
+  *ws_out = ws;
+  return iout;
+}
+
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
                  uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr) {
   if (nblocks == 0) return SF_OK;
-  const uint64_t maxb = launch_max_blocks();
+  const bool sorted = nblocks >= table_sort_min();
+  const uint64_t maxb = sorted ? std::min(launch_max_blocks(), kSortMaxBlocks) : launch_max_blocks();
   if (nblocks > maxb) {  // consecutive pieces of the table, one launch each
     for (uint64_t first = 0; first < nblocks; first += maxb) {
       const int rc = launch_table(d_data, len, d_offsets + first, d_sizes + first, std::min(maxb, nblocks - first),
@@ -136,15 +189,19 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
     return SF_OK;
   }
   const unsigned grid = grid_for_blocks(nblocks);
+  void* ws = nullptr;
+  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
   if (weak)
     hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, true>), dim3(grid), dim3(sf::kThreads), 0, stream,
                        static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, weak);
+                       static_cast<uint8_t*>(d_digests), d_status, weak, order);
   else
     hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, false>), dim3(grid), dim3(sf::kThreads), 0, stream,
                        static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, nullptr);
-  return hip_err(hipGetLastError());
+                       static_cast<uint8_t*>(d_digests), d_status, nullptr, order);
+  const int rc = hip_err(hipGetLastError());
+  if (ws) (void)hipFreeAsync(ws, stream);
+  return rc;
 }
 
 // Many equal-size, block-aligned files back to back, with their per-file

@@ -77,6 +77,12 @@ __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
   return v;
 }
 
+// 64 bytes at any byte address (four 16-B loads; unaligned global access).
+__device__ __forceinline__ void ld_chunk_any(uint4 (&v)[4], const uint8_t* p) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) __builtin_memcpy(&v[q], p + 16 * q, 16);
+}
+
 // Number of SHA-1 compressions for a message of `size` bytes.
 __device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
 
@@ -285,15 +291,24 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 #undef SF_ISSUE
     c_done = nsteps * CH;
   } else {
-    // Misaligned or > 4 GiB span: each lane streams its own block.
+    // Misaligned or > 4 GiB span: each lane streams its own block, 64 B per
+    // compression with four (unaligned) 16-B loads, the next chunk's loads
+    // in flight while the current one is compressed.
     const uint8_t* p = data + off;
+    uint4 nx[4];
+    if (nfull) ld_chunk_any(nx, p);
     for (uint32_t c = 0; c < nfull; ++c) {
       uint32_t le[16], w[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        le[j] = ld_u32_any(p + (uint64_t)c * 64 + 4 * j);
-        w[j] = bswap32(le[j]);
+      for (int q = 0; q < 4; ++q) {
+        le[4 * q + 0] = nx[q].x;
+        le[4 * q + 1] = nx[q].y;
+        le[4 * q + 2] = nx[q].z;
+        le[4 * q + 3] = nx[q].w;
       }
+      if (c + 1 < nfull) ld_chunk_any(nx, p + (uint64_t)(c + 1) * 64);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = bswap32(le[j]);
       if constexpr (WEAK) wk.chunk(le);
       st.compress(w);
     }
@@ -746,18 +761,25 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
 // many-file batches, and (over the digest table) per-file blocks_hash.
 // A block outside [0, len) is not read: its digest is zeroed and *status is
 // set to -34 (SF_ERANGE).
+// `order` (optional): the blocks in the order the waves take them -- wave w
+// hashes blocks order[64w .. 64w+63] and writes each digest at the block's
+// own index.  The launcher passes the blocks sorted by compression count,
+// largest first: a wave runs as long as its longest block, so a list of
+// mixed sizes (content-defined blocks, files' short last blocks) wastes
+// most lanes unless each wave's 64 blocks are about the same length; and
+// handing out the longest blocks first keeps the grid's tail short (LPT).
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(kThreads)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
-                  int* __restrict__ status, uint32_t* __restrict__ weak) {
+                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
   if (first >= nblocks) return;
-  const uint64_t blk = first + lane;
-  bool valid = blk < nblocks;
+  bool valid = first + lane < nblocks;
+  const uint64_t blk = (order && valid) ? (uint64_t)order[first + lane] : first + lane;
   uint64_t off = 0;
   uint32_t size = 0;
   bool bad = false;
@@ -798,6 +820,19 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
       if constexpr (WEAK) weak[blk] = wk.fin();
     }
   }
+}
+
+// Sort keys of an explicit block list for sha1_table_kernel's `order`: the
+// block's compression count (clamped to 16 bits: blocks of >= 4 MiB sort
+// together) and its index.
+__global__ void __launch_bounds__(256)
+table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __restrict__ keys,
+                  uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = n_chunks(sizes[i]);
+  keys[i] = (uint16_t)(c < 0xFFFFu ? c : 0xFFFFu);
+  idx[i] = (uint32_t)i;
 }
 
 // Wire emission of the signature table as the reference's FILE_BLOCK

@@ -1,0 +1,161 @@
+"""GPU: explicit block lists hashed in order of length (sha1_table_kernel's
+`order`, launch_table's rocprim sort).
+
+The launcher sorts a list of >= 2^17 blocks by compression count, largest
+first, so each wave's 64 blocks are about the same length; every digest must
+still land at its block's own index, bit-identical to the oracle
+(src/index.rs:621-647 restated) and to the list-order launch.
+SF_TABLE_SORT=1 forces the sorted launch on small lists, SF_TABLE_SORT=0 the
+list order."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from syncfast_amd import device
+from syncfast_amd._lib import SfError
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(data, gpu, shift=0):
+    t = torch.empty(data.size + shift, dtype=torch.uint8, device=gpu)
+    if data.size:
+        t[shift:] = torch.from_numpy(data).to(gpu)
+    return t[shift:]
+
+
+def _cdc_like(rng, n, mean=8192, cap=32768):
+    """Content-defined-like boundaries: geometric sizes (mean 8 KiB), capped
+    at 32 KiB (ZPAQ 13 bits + max_size, src/index.rs:40-41), tiling [0, n)."""
+    sizes = np.minimum(cap, np.maximum(1, rng.geometric(1 / mean, size=n // 64 + 16))).astype(np.int64)
+    ends = np.cumsum(sizes)
+    k = int(np.searchsorted(ends, n))
+    sizes = sizes[:k + 1]
+    sizes[-1] = n - (int(ends[k - 1]) if k else 0)
+    sizes = sizes[sizes > 0]
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    return offs, sizes
+
+
+@pytest.mark.parametrize("case", range(60))
+def test_sorted_explicit_blocks_fuzz(gpu, case, monkeypatch):
+    # random, overlapping, unsorted, empty and tiny-to-70 KB blocks, any
+    # alignment of the data pointer: forced sort, then list order
+    rng = np.random.default_rng(31_000 + case)
+    n = int(rng.integers(0, 2 << 20))
+    data = oracle.splitmix_bytes(n, 41_000 + case)
+    m = int(rng.integers(0, 700))
+    sizes = np.minimum(rng.integers(0, 70_000, m).astype(np.int64), n)
+    offs = np.array([int(rng.integers(0, n - s + 1)) for s in sizes], np.int64)
+    t = _dev(data, gpu, int(rng.integers(0, 16)))
+    to, tz = torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu)
+    want = oracle.index_blocks(data, offs, sizes)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SF_TABLE_SORT", mode)
+        got = device.index_device_blocks(t, to, tz).cpu().numpy()
+        assert np.array_equal(got, want), (mode, n, m)
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_sorted_cdc_like_lists(gpu, case, monkeypatch):
+    rng = np.random.default_rng(32_000 + case)
+    n = int(rng.integers(1, 24 << 20))
+    data = oracle.splitmix_bytes(n, 42_000 + case)
+    offs, sizes = _cdc_like(rng, n)
+    assert offs[-1] + sizes[-1] == n
+    t = _dev(data, gpu, int(rng.integers(0, 16)))
+    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    got = device.index_device_blocks(t, torch.from_numpy(offs).to(gpu),
+                                     torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
+    assert np.array_equal(got, oracle.index_blocks(data, offs, sizes)), (n, offs.size)
+
+
+def test_sorted_out_of_range_blocks(gpu, monkeypatch):
+    # blocks outside the buffer sort like any other (by their claimed size)
+    # and still report SF_ERANGE with a zero digest at their own index
+    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    rng = np.random.default_rng(33_000)
+    n = 1 << 20
+    data = oracle.splitmix_bytes(n, 43_000)
+    offs, sizes = _cdc_like(rng, n)
+    bad = rng.choice(offs.size, 5, replace=False)
+    offs2, sizes2 = offs.copy(), sizes.copy()
+    offs2[bad[:3]] = n + 1
+    sizes2[bad[3:]] = n + 100
+    t = _dev(data, gpu)
+    to, tz = torch.from_numpy(offs2).to(gpu), torch.from_numpy(sizes2.astype(np.int32)).to(gpu)
+    with pytest.raises(SfError):
+        device.index_device_blocks(t, to, tz)
+    got = device.index_device_blocks(t, to, tz, check_range=False).cpu().numpy()
+    good = np.setdiff1d(np.arange(offs.size), bad)
+    want = oracle.index_blocks(data, offs[good], sizes[good])
+    assert np.array_equal(got[good], want)
+    assert not got[bad].any()
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_sorted_weak_blocks(gpu, case, monkeypatch):
+    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    rng = np.random.default_rng(34_000 + case)
+    n = int(rng.integers(1, 6 << 20))
+    data = oracle.splitmix_bytes(n, 44_000 + case)
+    offs, sizes = _cdc_like(rng, n, mean=4096)
+    t = _dev(data, gpu, int(rng.integers(0, 16)))
+    dig, weak = device.index_device_blocks_weak(t, torch.from_numpy(offs).to(gpu),
+                                                torch.from_numpy(sizes.astype(np.int32)).to(gpu))
+    assert np.array_equal(dig.cpu().numpy(), oracle.index_blocks(data, offs, sizes))
+    assert np.array_equal(weak.cpu().numpy().view(np.uint32), oracle.adler_blocks(data, offs, sizes))
+
+
+@pytest.mark.parametrize("case", range(20))
+def test_sorted_ragged_batch(gpu, case, monkeypatch):
+    # ragged many-file batches: the block table and the per-file blocks_hash
+    # table (one lane per file over runs of different lengths) both sorted
+    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    rng = np.random.default_rng(35_000 + case)
+    bs = int(rng.choice([64, 100, 4096, 4097, 65536]))
+    nf = int(rng.integers(1, 200))
+    lens = [int(rng.integers(0, 40 * bs)) for _ in range(nf)]
+    align = int(rng.choice([1, 16]))
+    files, off = [], 0
+    for ln in lens:
+        files.append((off, ln))
+        off += (ln + align - 1) // align * align
+    data = oracle.splitmix_bytes(off, 45_000 + case)
+    dig, first, fh = device.index_device_batch(_dev(data, gpu), files, bs)
+    dig, fh = dig.cpu().numpy(), fh.cpu().numpy()
+    for k, (o, ln) in enumerate(files):
+        want = oracle.index_fixed(data[o:o + ln], bs)[2]
+        assert np.array_equal(dig[first[k]:first[k + 1]], want), (k, ln, bs)
+        assert bytes(fh[k]) == oracle.blocks_hash(want), (k, ln, bs)
+
+
+def test_sorted_with_launch_split(gpu, monkeypatch):
+    # a list larger than one launch: each piece sorted on its own
+    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    monkeypatch.setenv("SF_LAUNCH_MAX_BLOCKS", "48")
+    rng = np.random.default_rng(36_000)
+    n = 3 << 20
+    data = oracle.splitmix_bytes(n, 46_000)
+    offs, sizes = _cdc_like(rng, n, mean=2048)
+    got = device.index_device_blocks(_dev(data, gpu, 3), torch.from_numpy(offs).to(gpu),
+                                     torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
+    assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
+
+
+def test_default_sort_large_cdc_list(gpu, monkeypatch):
+    # >= 2^17 blocks: the launcher sorts by itself; every digest equals the
+    # list-order launch and the oracle
+    monkeypatch.delenv("SF_TABLE_SORT", raising=False)
+    rng = np.random.default_rng(37_000)
+    n = 1 << 30
+    data = oracle.splitmix_bytes(n, 47_000)
+    offs, sizes = _cdc_like(rng, n)
+    assert offs.size >= 1 << 17
+    t = _dev(data, gpu, 5)
+    to, tz = torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu)
+    got = device.index_device_blocks(t, to, tz).cpu().numpy()
+    monkeypatch.setenv("SF_TABLE_SORT", "0")
+    assert np.array_equal(got, device.index_device_blocks(t, to, tz).cpu().numpy())
+    assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
