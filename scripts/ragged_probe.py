@@ -86,14 +86,29 @@ def main():
     cases["files"] = file_sizes(total, rng)
     # diagnostic: the per-lane (unaligned) load path with no size imbalance
     cases["list4k_unaligned"] = (offs4k[:-1] + 1, np.full(offs4k.size - 1, 4096, np.int64))
+    # diagnostic: the same unaligned 4 KiB blocks in a random order (every
+    # wave's 64 blocks far apart in memory, as in a length-sorted CDC list)
+    perm = rng.permutation(offs4k.size - 1)
+    cases["list4k_unaligned_shuffled"] = (offs4k[:-1][perm] + 1, np.full(offs4k.size - 1, 4096, np.int64))
+    if os.environ.get("PROBE_CLASS"):  # length-class width A/B on the CDC list (SF_TABLE_CLASS_BITS)
+        cases = {"cdc": cases["cdc"], "files": cases["files"]}
+    if os.environ.get("PROBE_ALIGN"):  # per-lane path at dword (+4) and 8-B (+8) alignment
+        cases = {}
+        for sh in (1, 4, 8):
+            cases[f"list4k_plus{sh}"] = (offs4k[:-1] + sh, np.full(offs4k.size - 1, 4096, np.int64))
     out = {}
     for rep in range(2):
         ms = timed(lambda: index_device(data, 4096, out=dig_fixed, stream=s), s)
         out["fixed4k"] = {"ms": round(ms, 3), "GiB/s": round(total / GiB / (ms * 1e-3), 1)}
-        for (name, (o, z)), srt in [(c, m) for c in cases.items() for m in ("0", "1")]:
+        modes = [("0", None), ("1", None)]
+        if os.environ.get("PROBE_CLASS"):
+            modes = [("1", b) for b in ("2", "3", "4", "5", "6")]
+        for (name, (o, z)), (srt, cb) in [(c, m) for c in cases.items() for m in modes]:
             # SF_TABLE_SORT: 0 = list order, 1 = blocks sorted by length (the default from 2^17 blocks)
             os.environ["SF_TABLE_SORT"] = srt
-            name = name + ("_sorted" if srt == "1" else "")
+            if cb:
+                os.environ["SF_TABLE_CLASS_BITS"] = cb
+            name = name + ("_sorted" if srt == "1" else "") + (f"_m{cb}" if cb else "")
             to = torch.from_numpy(o).to(dev)
             tz = torch.from_numpy(z.astype(np.int32)).to(dev)
             dig = torch.empty((o.size, 20), dtype=torch.uint8, device=dev)
@@ -103,7 +118,7 @@ def main():
                          "mean_block": round(nbytes / o.size, 1)}
             if rep == 0:
                 d = dig.cpu().numpy()
-                if name.startswith("list4k") and "unaligned" not in name:
+                if name in ("list4k", "list4k_sorted"):
                     assert np.array_equal(d, dig_fixed.cpu().numpy()), name
                 for i in rng.integers(0, o.size, 64):
                     b = data[int(o[i]): int(o[i]) + int(z[i])].cpu().numpy().tobytes()

@@ -137,18 +137,22 @@ inline uint64_t table_sort_min() {
   if (e) return atoi(e) ? 1 : ~0ull;
   return 1ull << 17;
 }
-constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.5 GiB of workspace at most)
+constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
 
 // Stream-ordered workspace holding the processing order of blocks [0, n) of
-// a list: stable radix sort of (compression count, index), descending, with
-// rocprim on `s`.  Returns nullptr (unsorted launch) if anything fails.
+// a list: stable radix sort of (length class, index) by class, descending,
+// with rocprim on `s` (one 8-bit key; list order within a class).  Returns
+// nullptr (unsorted launch) if anything fails.
 uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
   *ws_out = nullptr;
+  const char* me = getenv("SF_TABLE_CLASS_BITS");  // mantissa bits of the length class, 1..6 (A/B knob)
+  const uint32_t mbits = me ? (uint32_t)std::min(6, std::max(1, atoi(me))) : 6u;
+  const unsigned kbits = 5u + mbits;  // class < 32 << mbits
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   uint16_t *kin = nullptr, *kout = nullptr;
   uint32_t *iin = nullptr, *iout = nullptr;
   size_t tmp = 0;
-  if (rocprim::radix_sort_pairs_desc(nullptr, tmp, kin, kout, iin, iout, (unsigned)n, 0u, 16u, s) != hipSuccess) {
+  if (rocprim::radix_sort_pairs_desc(nullptr, tmp, kin, kout, iin, iout, (unsigned)n, 0u, kbits, s) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
@@ -162,9 +166,10 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   kout = reinterpret_cast<uint16_t*>(ws + kb);
   iin = reinterpret_cast<uint32_t*>(ws + 2 * kb);
   iout = reinterpret_cast<uint32_t*>(ws + 2 * kb + ib);
-  hipLaunchKernelGGL(sf::table_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, kin, iin);
+  hipLaunchKernelGGL(sf::table_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, kin, iin,
+                     mbits);
   if (hipGetLastError() != hipSuccess ||
-      rocprim::radix_sort_pairs_desc(ws + 2 * kb + 2 * ib, tmp, kin, kout, iin, iout, (unsigned)n, 0u, 16u, s) !=
+      rocprim::radix_sort_pairs_desc(ws + 2 * kb + 2 * ib, tmp, kin, kout, iin, iout, (unsigned)n, 0u, kbits, s) !=
           hipSuccess) {
     (void)hipGetLastError();
     (void)hipFreeAsync(ws, s);

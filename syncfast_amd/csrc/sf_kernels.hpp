@@ -83,6 +83,12 @@ __device__ __forceinline__ void ld_chunk_any(uint4 (&v)[4], const uint8_t* p) {
   for (int q = 0; q < 4; ++q) __builtin_memcpy(&v[q], p + 16 * q, 16);
 }
 
+// 64 bytes at a 4-B aligned address (four 16-B loads).
+__device__ __forceinline__ void ld_chunk_al(uint4 (&v)[4], const uint32_t* p) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) __builtin_memcpy(&v[k], p + 4 * k, 16);
+}
+
 // Number of SHA-1 compressions for a message of `size` bytes.
 __device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
 
@@ -193,7 +199,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
   st.init();
   if constexpr (WEAK) wk.init();
   const uint32_t nfull = geo.min_size / 64u;
-  uint32_t c_done = 0;
+  uint32_t c_done = 0;  // this lane's chunks done
   if (geo.lds_ok) {
     const uint32_t nsteps = nfull / CH;
     // Source offsets (relative to the span base) of this lane's 16-B piece in
@@ -291,28 +297,81 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
 #undef SF_ISSUE
     c_done = nsteps * CH;
   } else {
-    // Misaligned or > 4 GiB span: each lane streams its own block, 64 B per
-    // compression with four (unaligned) 16-B loads, the next chunk's loads
-    // in flight while the current one is compressed.
-    const uint8_t* p = data + off;
-    uint4 nx[4];
-    if (nfull) ld_chunk_any(nx, p);
-    for (uint32_t c = 0; c < nfull; ++c) {
-      uint32_t le[16], w[16];
+    if constexpr (HAS_PAD) {
+      // (fixed tiling, only for a misaligned data pointer or block size: the
+      // hot kernel's code -- any change here moves its register assignment,
+      // and one such move cost the headline launch 3.7 %)
+      // Misaligned or > 4 GiB span: each lane streams its own block, 64 B per
+      // compression with four (unaligned) 16-B loads, the next chunk's loads
+      // in flight while the current one is compressed.
+      const uint8_t* p = data + off;
+      uint4 nx[4];
+      if (nfull) ld_chunk_any(nx, p);
+      for (uint32_t c = 0; c < nfull; ++c) {
+        uint32_t le[16], w[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        le[4 * q + 0] = nx[q].x;
-        le[4 * q + 1] = nx[q].y;
-        le[4 * q + 2] = nx[q].z;
-        le[4 * q + 3] = nx[q].w;
+        for (int q = 0; q < 4; ++q) {
+          le[4 * q + 0] = nx[q].x;
+          le[4 * q + 1] = nx[q].y;
+          le[4 * q + 2] = nx[q].z;
+          le[4 * q + 3] = nx[q].w;
+        }
+        if (c + 1 < nfull) ld_chunk_any(nx, p + (uint64_t)(c + 1) * 64);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap32(le[j]);
+        if constexpr (WEAK) wk.chunk(le);
+        st.compress(w);
       }
-      if (c + 1 < nfull) ld_chunk_any(nx, p + (uint64_t)(c + 1) * 64);
+      c_done = nfull;
+    } else {
+      // Misaligned or > 4 GiB span: each lane streams its own block, 64 B per
+      // compression, the next chunk's loads in flight while the current one is
+      // compressed, up to ITS OWN last whole chunk (lanes whose block has fewer
+      // whole chunks than the wave's longest idle meanwhile).  Loads are
+      // dword-aligned (a byte-aligned 16-B load costs the address unit several
+      // times over: 4 KiB blocks at byte offset +1 ran at 1911 GiB/s, at +4 at
+      // 2832, scripts/ragged_probe.py): the lane reads 17 dwords from its block
+      // start rounded down to 4 B and shifts the message words out of them
+      // (v_alignbyte by the lane's byte offset r).  Every dword read holds at
+      // least one byte of the block, so nothing is touched outside the dwords
+      // the block's bytes lie in.
+      const uint8_t* p = data + off;
+      const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(p - r);
+      const uint32_t mine = valid ? size / 64u : 0u;  // this lane's whole chunks
+      const uint32_t upto = geo.max_size / 64u;       // the wave's most
+      uint4 nx[4];
+      uint32_t nx16 = 0u;  // dword 16 of the chunk in nx (needed when r != 0)
+      if (mine) {
+        ld_chunk_al(nx, q);
+        if (r != 0u || mine > 1) nx16 = q[16];
+      }
+      for (uint32_t c = 0; c < upto; ++c) {
+        if (c < mine) {
+          uint32_t d[17], le[16], w[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = bswap32(le[j]);
-      if constexpr (WEAK) wk.chunk(le);
-      st.compress(w);
+          for (int k = 0; k < 4; ++k) {
+            d[4 * k + 0] = nx[k].x;
+            d[4 * k + 1] = nx[k].y;
+            d[4 * k + 2] = nx[k].z;
+            d[4 * k + 3] = nx[k].w;
+          }
+          d[16] = nx16;
+          if (c + 1 < mine) {
+            ld_chunk_al(nx, q + 16 * (uint64_t)(c + 1));
+            if (r != 0u || c + 2 < mine) nx16 = q[16 * (uint64_t)(c + 2)];
+          }
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            le[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], r);
+            w[j] = bswap32(le[j]);
+          }
+          if constexpr (WEAK) wk.chunk(le);
+          st.compress(w);
+        }
+      }
+      c_done = mine;
     }
-    c_done = nfull;
   }
   // Weak sum of this lane's bytes past the chunks both paths consumed
   // (whole chunks, then < 64 single bytes); never reads outside the block.
@@ -769,7 +828,7 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
 // most lanes unless each wave's 64 blocks are about the same length; and
 // handing out the longest blocks first keeps the grid's tail short (LPT).
 template <int TILE, bool WEAK = false>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 3)  // 3 waves/SIMD, as the fixed kernel (the weak form asked 169 VGPRs)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
                   int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order) {
@@ -823,15 +882,25 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 }
 
 // Sort keys of an explicit block list for sha1_table_kernel's `order`: the
-// block's compression count (clamped to 16 bits: blocks of >= 4 MiB sort
-// together) and its index.
+// block's compression count on a log scale with 3 mantissa bits (classes
+// 6-12 % wide; exact below 8), and its index.  A class holds many blocks, so
+// a wave's 64 blocks (consecutive in the stable sort: list order within a
+// class) lie close together in memory; an exact-count key spreads them over
+// the whole buffer (every nch value is rare), and 64 lanes streaming from 64
+// far-apart places run memory-bound: 4 KiB blocks in a shuffled order hashed
+// at 1200 GiB/s against 2857 in order (scripts/ragged_probe.py).
+__device__ __forceinline__ uint16_t length_class(uint32_t nch, uint32_t mbits) {
+  if (nch < (1u << mbits)) return (uint16_t)nch;
+  const uint32_t e = 31u - (uint32_t)__builtin_clz(nch);  // floor(log2), >= mbits
+  return (uint16_t)((e << mbits) + ((nch >> (e - mbits)) & ((1u << mbits) - 1u)));  // < 32 << mbits
+}
+
 __global__ void __launch_bounds__(256)
 table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __restrict__ keys,
-                  uint32_t* __restrict__ idx) {
+                  uint32_t* __restrict__ idx, uint32_t mbits) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t c = n_chunks(sizes[i]);
-  keys[i] = (uint16_t)(c < 0xFFFFu ? c : 0xFFFFu);
+  keys[i] = length_class(n_chunks(sizes[i]), mbits);
   idx[i] = (uint32_t)i;
 }
 
