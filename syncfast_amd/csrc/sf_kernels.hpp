@@ -873,7 +873,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
       uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);
       o[0] = o[1] = o[2] = o[3] = o[4] = 0;
       if constexpr (WEAK) weak[blk] = 0u;
-      if (status) *status = -34;
+      if (status) *status = SF_ERANGE;
     } else {
       st.store(digests + blk * 20);
       if constexpr (WEAK) weak[blk] = wk.fin();
@@ -882,8 +882,8 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 }
 
 // Sort keys of an explicit block list for sha1_table_kernel's `order`: the
-// block's compression count on a log scale with 3 mantissa bits (classes
-// 6-12 % wide; exact below 8), and its index.  A class holds many blocks, so
+// block's compression count on a log scale with `mbits` mantissa bits (the
+// launcher's default 6: classes <= 1.6 % wide, exact below 64), and its index.  A class holds many blocks, so
 // a wave's 64 blocks (consecutive in the stable sort: list order within a
 // class) lie close together in memory; an exact-count key spreads them over
 // the whole buffer (every nch value is rare), and 64 lanes streaming from 64
