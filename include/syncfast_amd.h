@@ -209,6 +209,25 @@ int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t s
 int sf_index_buffer(const uint8_t *data, uint64_t len, uint32_t block_size,
                     sf_block_sig *out, uint64_t cap, uint64_t *n_out);
 
+/* End to end from host memory with an explicit block list: block i =
+ * data[offsets[i], offsets[i] + sizes[i]) -- the boundaries a chunker on the
+ * host produced (the reference's default is cdchunking's ZPAQ,
+ * src/index.rs:622-625: a Rust caller keeps that crate, runs it over the
+ * file's bytes and hands the bytes + boundaries here).  Replaces the
+ * Sha1::update / digest loop of src/index.rs:628-644 for every block.
+ * Blocks must be in non-decreasing offset order (a chunker's output; they
+ * may overlap and need not cover the buffer); sizes may be 0 (SHA-1 of no
+ * bytes).  The list is checked before anything runs: SF_ERANGE if a block
+ * passes len, SF_EINVAL if the offsets go backwards.  Stages of about
+ * 256 MiB of whole blocks are copied (16 threads) into pinned buffers, moved
+ * to HBM with their part of the list and hashed by the explicit-list kernel
+ * while the next stage is copied.  out[i] = {offsets[i], sizes[i], digest};
+ * blocks_hash (may be NULL) = SHA-1 over the digests in list order
+ * (compute_blocks_hash, src/index.rs:661-682).  n_blocks rows; blocking. */
+int sf_index_buffer_blocks(const uint8_t *data, uint64_t len, const uint64_t *offsets,
+                           const uint32_t *sizes, uint64_t n_blocks, sf_block_sig *out,
+                           uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
 /* End to end from a file on disk (the reference's input, src/index.rs:615):
  * pread into pinned buffers, overlapped H2D + kernel, D2H.  Writes the
  * rows and the file's blocks_hash.  Blocking.  A path that cannot seek (FIFO,

@@ -180,7 +180,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
 }
 
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
-                 uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr) {
+                 uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak) {
   if (nblocks == 0) return SF_OK;
   const bool sorted = nblocks >= table_sort_min();
   const uint64_t maxb = sorted ? std::min(launch_max_blocks(), kSortMaxBlocks) : launch_max_blocks();

@@ -505,9 +505,152 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
   return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
 }
 
+// Copy n bytes into a pinned stage with several threads (one thread moves
+// ~10-16 GB/s, below the PCIe link the stage is waiting for).
+inline void par_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
+  const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(n, nthreads));
+  const uint64_t nslices = ceil_div(n, slice);
+  if (nslices <= 1) {
+    if (n) memcpy(dst, src, n);
+    return;
+  }
+  std::atomic<uint64_t> next{0};
+  run_pool((unsigned)std::min<uint64_t>(nthreads, nslices), [&] {
+    for (uint64_t i; (i = next.fetch_add(1)) < nslices;) {
+      const uint64_t a = i * slice, b = std::min(n, a + slice);
+      memcpy(dst + a, src + a, b - a);
+    }
+  });
+}
+
+// One stage of an explicit block list: blocks [b0, b1), whose bytes all lie
+// in the window [w0, w1) of the caller's buffer.
+struct ListStage {
+  uint64_t b0, b1, w0, w1;
+};
+constexpr uint64_t kListStageMaxBlocks = 1ull << 22;  // keeps a stage's list and digests (~135 MiB) bounded
+
+// sf_index_buffer_blocks: the list is cut into stages of consecutive blocks
+// whose window spans at most ~256 MiB (a larger block is a stage of its own);
+// per stage, on alternating streams: the window and the stage's list
+// (offsets relative to the window, sizes) are copied into pinned buffers and
+// to HBM, sha1_table_kernel hashes the blocks, the digests come back.  While
+// stage k is copied in, stage k-1 is on the device and stage k-2's rows are
+// written and folded into blocks_hash, in list order.
+static int index_list_pipeline(const uint8_t* data, const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                               sf_block_sig* out, uint8_t* blocks_hash) {
+  const uint64_t target = file_stage_bytes(1);  // ~256 MiB (SF_STREAM_STAGE_MIB test knob)
+  std::vector<ListStage> stages;
+  uint64_t max_win = 0, max_blocks = 0;
+  for (uint64_t i = 0; i < n;) {
+    ListStage s{i, i + 1, offsets[i], offsets[i] + sizes[i]};
+    for (i++; i < n && i - s.b0 < kListStageMaxBlocks; i++) {
+      const uint64_t e = std::max(s.w1, offsets[i] + sizes[i]);
+      if (e - s.w0 > target) break;
+      s.w1 = e;
+    }
+    s.b1 = i;
+    max_win = std::max(max_win, s.w1 - s.w0);
+    max_blocks = std::max(max_blocks, s.b1 - s.b0);
+    stages.push_back(s);
+  }
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done;
+  void *ddata[2], *pin[2], *dlist[2], *plist[2], *ddig[2], *pdig[2];
+  const uint64_t list_bytes = max_blocks * (sizeof(uint64_t) + sizeof(uint32_t));
+  int rc = res.streams(st, done);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, max_win, &ddata[i]);
+    if (rc == SF_OK) rc = res.pin(i, max_win, &pin[i]);
+    if (rc == SF_OK) rc = res.dev(3 + i, max_blocks * 20, &ddig[i]);
+    if (rc == SF_OK) rc = res.pin(3 + i, max_blocks * 20, &pdig[i]);
+    if (rc == SF_OK) rc = res.dev(5 + i, list_bytes, &dlist[i]);
+    if (rc == SF_OK) rc = res.pin(5 + i, list_bytes, &plist[i]);
+  }
+  if (rc != SF_OK) return rc;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  int64_t stage_of[2] = {-1, -1};  // stage in flight on each buffer set
+  auto harvest = [&](int b) {
+    if (hipEventSynchronize(done[b]) != hipSuccess) return SF_ENODEV;
+    const ListStage& s = stages[(size_t)stage_of[b]];
+    stage_of[b] = -1;
+    const uint8_t* dg = static_cast<const uint8_t*>(pdig[b]);
+    for (uint64_t i = s.b0; i < s.b1; i++) {
+      out[i].offset = offsets[i];
+      out[i].size = sizes[i];
+      memcpy(out[i].sha1, dg + 20 * (i - s.b0), 20);
+    }
+    if (blocks_hash) sf_host_sha1_update(&bh, dg, (s.b1 - s.b0) * 20);
+    return SF_OK;
+  };
+  for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (stage_of[b] >= 0 && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (k-1 comes later in list order)
+    const ListStage& s = stages[k];
+    const uint64_t nb = s.b1 - s.b0, win = s.w1 - s.w0;
+    par_memcpy(static_cast<uint8_t*>(pin[b]), data + s.w0, win);
+    uint64_t* lo = static_cast<uint64_t*>(plist[b]);
+    uint32_t* lz = reinterpret_cast<uint32_t*>(lo + nb);
+    for (uint64_t i = 0; i < nb; i++) {
+      lo[i] = offsets[s.b0 + i] - s.w0;
+      lz[i] = sizes[s.b0 + i];
+    }
+    const uint64_t* d_off = static_cast<const uint64_t*>(dlist[b]);
+    const uint32_t* d_sz = reinterpret_cast<const uint32_t*>(d_off + nb);
+    if ((win && hipMemcpyAsync(ddata[b], pin[b], win, hipMemcpyHostToDevice, st[b]) != hipSuccess) ||
+        hipMemcpyAsync(dlist[b], plist[b], nb * (sizeof(uint64_t) + sizeof(uint32_t)), hipMemcpyHostToDevice,
+                       st[b]) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+    // every block was checked to lie in [0, len), so in its window: no status word
+    if ((rc = launch_table(ddata[b], win, d_off, d_sz, nb, ddig[b], nullptr, st[b])) != SF_OK) break;
+    if (hipMemcpyAsync(pdig[b], ddig[b], nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(done[b], st[b]) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+    stage_of[b] = (int64_t)k;
+  }
+  // the (at most two) stages still in flight, in list order
+  int order[2] = {0, 1};
+  if (stage_of[0] >= 0 && stage_of[1] >= 0 && stage_of[1] < stage_of[0]) std::swap(order[0], order[1]);
+  for (int b : order)
+    if (stage_of[b] >= 0) {
+      const int r = harvest(b);
+      if (rc == SF_OK) rc = r;
+    }
+  if (rc == SF_OK && blocks_hash) sf_host_sha1_final(&bh, blocks_hash);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
+
+static int sf_index_buffer_blocks_body(const uint8_t* data, uint64_t len, const uint64_t* offsets,
+                                       const uint32_t* sizes, uint64_t n, sf_block_sig* out, uint8_t* blocks_hash) {
+  if (n && (!offsets || !sizes || !out)) return SF_EINVAL;
+  if (len && !data) return SF_EINVAL;
+  // The whole list is checked before any byte moves (the device form zeroes
+  // an out-of-range block's digest instead; a host caller gets the error).
+  for (uint64_t i = 0; i < n; i++) {
+    if (offsets[i] > len || sizes[i] > len - offsets[i]) return SF_ERANGE;
+    if (i && offsets[i] < offsets[i - 1]) return SF_EINVAL;
+  }
+  if (n == 0) {
+    if (blocks_hash) {  // compute_blocks_hash of no blocks: SHA-1 of the empty string
+      sf_host_sha1_stream bh;
+      sf_host_sha1_begin(&bh);
+      sf_host_sha1_final(&bh, blocks_hash);
+    }
+    return SF_OK;
+  }
+  return index_list_pipeline(data, offsets, sizes, n, out, blocks_hash);
+}
 
 static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
@@ -692,6 +835,11 @@ int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t bl
 int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
                     uint64_t* n_out) {
   return guarded([&] { return sf_index_buffer_body(data, len, block_size, out, cap, n_out); });
+}
+
+int sf_index_buffer_blocks(const uint8_t* data, uint64_t len, const uint64_t* offsets, const uint32_t* sizes,
+                           uint64_t n_blocks, sf_block_sig* out, uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_buffer_blocks_body(data, len, offsets, sizes, n_blocks, out, blocks_hash); });
 }
 
 int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,

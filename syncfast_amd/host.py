@@ -38,6 +38,27 @@ def index_buffer(data, block_size: int) -> np.ndarray:
     return out[:n]
 
 
+def index_buffer_blocks(data, offsets, sizes) -> Tuple[np.ndarray, bytes]:
+    """Signatures of an explicit block list over a host buffer (block i =
+    data[offsets[i]:offsets[i]+sizes[i]], offsets non-decreasing: a chunker's
+    output) -> (SIG_DTYPE rows in list order, blocks_hash over their digests)
+    (sf_index_buffer_blocks).  SF_ERANGE / SF_EINVAL for a block past the end
+    / offsets that go backwards, before anything runs."""
+    a = _u8(data)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
+    szs = np.ascontiguousarray(sizes, dtype=np.uint32).reshape(-1)
+    if offs.size != szs.size:
+        raise ValueError("offsets and sizes differ in length")
+    n = offs.size
+    out = np.zeros(max(n, 1), SIG_DTYPE)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_buffer_blocks(a.ctypes.data if a.size else None, a.size,
+                                       offs.ctypes.data if n else None, szs.ctypes.data if n else None, n,
+                                       out.ctypes.data_as(ctypes.POINTER(BlockSig)), bh),
+          "sf_index_buffer_blocks")
+    return out[:n], bytes(bh)
+
+
 def release_cache() -> None:
     """Free the streams and buffers the host entry points keep between calls
     (sf_release_host_cache)."""

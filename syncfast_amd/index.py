@@ -160,22 +160,19 @@ def signatures_of_bytes(data, chunker) -> List[Tuple[int, int, bytes]]:
     if isinstance(chunker, FixedChunker):
         return host.rows_to_tuples(host.index_buffer(data, chunker.block_size))
     if isinstance(chunker, BoundaryChunker):
-        import torch
-        from . import device
+        # the boundaries come from the host-side chunker, as the reference's
+        # do (src/index.rs:622-625); every block's SHA-1 is computed on the
+        # device through the host-memory C-ABI entry (sf_index_buffer_blocks)
         raw = bytes(data)
         sizes = [int(s) for s in chunker.fn(raw)]
         if any(s <= 0 for s in sizes) or sum(sizes) != len(raw):
             raise ValueError("boundary function must return positive sizes covering the data")
-        offs = np.zeros(len(sizes), np.int64)
-        if sizes:
-            offs[1:] = np.cumsum(sizes)[:-1]
         if not sizes:
             return []
-        dev = torch.device("cuda", torch.cuda.current_device())
-        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-        dig = device.index_device_blocks(t, torch.from_numpy(offs).to(dev),
-                                         torch.tensor(sizes, dtype=torch.int32, device=dev)).cpu().numpy()
-        return [(int(o), int(s), bytes(d)) for o, s, d in zip(offs, sizes, dig)]
+        offs = np.zeros(len(sizes), np.uint64)
+        offs[1:] = np.cumsum(sizes, dtype=np.uint64)[:-1]
+        rows, _ = host.index_buffer_blocks(raw, offs, np.asarray(sizes, np.uint32))
+        return host.rows_to_tuples(rows)
     raise TypeError("unknown chunker")
 
 

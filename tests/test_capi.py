@@ -64,6 +64,36 @@ def test_argument_validation_without_device():
     assert L.sf_blocks_hash(None, 0, None) == _lib.SF_EINVAL
 
 
+def test_buffer_blocks_validation_without_device():
+    """sf_index_buffer_blocks checks the whole list before anything moves:
+    an empty list is the empty blocks_hash, a block past the end is SF_ERANGE
+    (the device form zeroes it instead), offsets going backwards SF_EINVAL."""
+    L = syncfast_amd.lib()
+    data = np.arange(100, dtype=np.uint8)
+    out = np.zeros(4, host.SIG_DTYPE)
+    pout = out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig))
+    bh = (ctypes.c_uint8 * 20)()
+    assert L.sf_index_buffer_blocks(data.ctypes.data, data.size, None, None, 0, None, bh) == 0
+    assert bytes(bh) == hashlib.sha1(b"").digest()
+    rows, h = host.index_buffer_blocks(b"", [], [])
+    assert rows.size == 0 and h == hashlib.sha1(b"").digest()
+
+    def call(offs, sizes, length=data.size):
+        o = np.asarray(offs, np.uint64)
+        s = np.asarray(sizes, np.uint32)
+        return L.sf_index_buffer_blocks(data.ctypes.data, length, o.ctypes.data, s.ctypes.data, o.size, pout, None)
+
+    assert call([0, 90], [10, 11]) == _lib.SF_ERANGE  # 90 + 11 > 100
+    assert call([101], [0]) == _lib.SF_ERANGE
+    assert call([0, 50, 40], [10, 10, 10]) == _lib.SF_EINVAL  # offsets go backwards
+    assert call([0], [1], length=0) == _lib.SF_ERANGE
+    assert L.sf_index_buffer_blocks(None, 10, None, None, 0, None, None) == _lib.SF_EINVAL  # len > 0, no data
+    o = np.zeros(1, np.uint64)
+    assert L.sf_index_buffer_blocks(data.ctypes.data, data.size, o.ctypes.data, None, 1, pout, None) == _lib.SF_EINVAL
+    with pytest.raises(_lib.SfError):
+        host.index_buffer_blocks(data, [0, 95], [10, 10])
+
+
 def test_host_paths_without_device():
     """Without a GPU the host-memory entry points fail cleanly: the in-place
     route (>= 1 MiB) cannot page-lock, the staged route cannot set up its
@@ -79,6 +109,11 @@ def test_host_paths_without_device():
     rc = L.sf_index_buffer(data.ctypes.data, data.size, 4096, out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)),
                            out.size, ctypes.byref(n))
     assert rc == _lib.SF_ENODEV and n.value == out.size
+    offs = np.arange(0, data.size, 8192, dtype=np.uint64)
+    sizes = np.full(offs.size, 8192, np.uint32)
+    rc = L.sf_index_buffer_blocks(data.ctypes.data, data.size, offs.ctypes.data, sizes.ctypes.data, offs.size,
+                                  out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)), None)
+    assert rc == _lib.SF_ENODEV
     assert L.sf_release_host_cache() == 0
 
 
