@@ -12,7 +12,9 @@
  *      -Wl,-rpath,$PWD/syncfast_amd/lib -o sf_index
  *   ./sf_index [-b block_size] [-m | -B | -s N] path...
  *     -m: all paths through one sf_index_files call; -B: each file from a host
- *     buffer (sf_index_buffer); -s N: each file as N sf_index_file_range shards;
+ *     buffer (sf_index_buffer); -C: each file cut by a content-defined chunker
+ *     on the host, its blocks hashed by sf_index_buffer_blocks;
+ *     -s N: each file as N sf_index_file_range shards;
  *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
  *     -L dst src: src's blocks looked up among dst's (sf_block_set_*)
  */
@@ -123,6 +125,55 @@ static int index_buffer_or_shards(const char *path, uint32_t bs, int shards) {
     return rc;
 }
 
+/* -C: content-defined blocks from C, the way the reference's default mode
+ * drops in (INTEGRATION.md index_file_rows_cdc): a chunker on the host cuts
+ * the file's bytes and sf_index_buffer_blocks hashes every block on the
+ * device.  The chunker here is a stand-in (the reference's cdchunking ZPAQ
+ * is Rust): a block ends after byte i when the little-endian word of bytes
+ * i-3..i, times 2654435761 (mod 2^32), is below 2^19 (rate 2^-13, ~8 KiB
+ * blocks), or when it reaches 32 KiB (src/index.rs:40-41). */
+static int index_cdc(const char *path) {
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;
+    const uint64_t len = (uint64_t)sb.st_size;
+    uint8_t *buf = malloc(len ? len : 1), bh[20];
+    uint64_t n = 0, cap = len / 4096 + 16;
+    uint64_t *offs = malloc(cap * sizeof(uint64_t));
+    uint32_t *sizes = malloc(cap * sizeof(uint32_t));
+    sf_block_sig *rows = NULL;
+    int rc = (buf && offs && sizes) ? SF_OK : SF_ENOMEM;
+    FILE *f = rc == SF_OK ? fopen(path, "rb") : NULL;
+    if (rc == SF_OK && (!f || fread(buf, 1, len, f) != len)) rc = SF_EIO;
+    if (f) fclose(f);
+    for (uint64_t start = 0, i = 0; rc == SF_OK && i < len; i++) {
+        const uint32_t w = i >= 3 ? (uint32_t)buf[i - 3] | (uint32_t)buf[i - 2] << 8 | (uint32_t)buf[i - 1] << 16 |
+                                        (uint32_t)buf[i] << 24
+                                  : 0xFFFFFFFFu;
+        if ((uint32_t)(w * 2654435761u) < (1u << 19) || i + 1 - start == 32768 || i + 1 == len) {
+            if (n == cap) {  /* the list grows as the chunker finds blocks */
+                uint64_t *o2 = realloc(offs, 2 * cap * sizeof(uint64_t));
+                if (o2) offs = o2;
+                uint32_t *s2 = o2 ? realloc(sizes, 2 * cap * sizeof(uint32_t)) : NULL;
+                if (s2) sizes = s2;
+                if (!o2 || !s2) { rc = SF_ENOMEM; break; }
+                cap *= 2;
+            }
+            offs[n] = start;
+            sizes[n] = (uint32_t)(i + 1 - start);
+            n++;
+            start = i + 1;
+        }
+    }
+    if (rc == SF_OK) rc = (rows = malloc((n ? n : 1) * sizeof(sf_block_sig))) ? SF_OK : SF_ENOMEM;
+    if (rc == SF_OK) rc = sf_index_buffer_blocks(buf, len, offs, sizes, n, rows, bh);
+    if (rc == SF_OK) print_rows(path, rows, n, bh);
+    free(buf);
+    free(offs);
+    free(sizes);
+    free(rows);
+    return rc;
+}
+
 /* -w N: the device-resident path and the wire stream from C: N bytes of the
  * splitmix64 stream (seed 0x5EED0000) generated in HBM
  * (sf_fill_splitmix_device), hashed there (sf_index_device_fixed), and the
@@ -224,7 +275,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0, buffer = 0, shards = 0, lookup = 0;
+    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0;
     long long wire = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -234,10 +285,11 @@ int main(int argc, char **argv) {
         else if (strcmp(argv[i], "-m") == 0) many = 1;
         else if (strcmp(argv[i], "-L") == 0) lookup = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
+        else if (strcmp(argv[i], "-C") == 0) cdc = 1;
         else break;
     }
     if (i >= argc && wire < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -s shards] path... | -w bytes | -L dst src\n",
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -s shards] path... | -w bytes | -L dst src\n",
                 argv[0]);
         return 2;
     }
@@ -266,8 +318,9 @@ int main(int argc, char **argv) {
         return status;
     }
     for (; i < argc; i++) {
-        const int rc = (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)
-                                              : index_one(argv[i], bs);
+        const int rc = cdc ? index_cdc(argv[i])
+                       : (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)
+                                                : index_one(argv[i], bs);
         if (rc != SF_OK) {
             fprintf(stderr, "%s: %s\n", argv[i], sf_strerror(rc));
             status = 1;

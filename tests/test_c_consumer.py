@@ -112,3 +112,54 @@ def test_c_consumer_block_lookup(gpu, tmp_path):
     got = [int(ln.split()[1]) for ln in r.stdout.decode().splitlines()]
     want = oracle.block_lookup(oracle.index_fixed(a.reshape(-1), bs)[2], None, oracle.index_fixed(b.reshape(-1), bs)[2])
     assert got == want.tolist() and sum(g >= 0 for g in got) == 150
+
+
+def _cdc_cuts(data: np.ndarray):
+    """The C consumer's stand-in chunker (-C), restated: a block ends after
+    byte i when the little-endian word of bytes i-3..i times 2654435761
+    (mod 2^32) is below 2^19, or at 32 KiB, or at the end of the data."""
+    n = data.size
+    trig = np.zeros(n, bool)
+    if n >= 4:
+        w = (data[:-3].astype(np.uint64) | data[1:-2].astype(np.uint64) << 8 |
+             data[2:-1].astype(np.uint64) << 16 | data[3:].astype(np.uint64) << 24)
+        trig[3:] = ((w * 2654435761) & 0xFFFFFFFF) < (1 << 19)
+    offs, sizes, start = [], [], 0
+    hits = np.flatnonzero(trig).tolist() + [n - 1]
+    k = 0
+    while start < n:
+        while hits[k] < start:
+            k += 1
+        end = min(hits[k], start + 32767, n - 1) + 1
+        offs.append(start)
+        sizes.append(end - start)
+        start = end
+    return offs, sizes
+
+
+@pytest.mark.gpu
+def test_c_consumer_content_defined_blocks(gpu, tmp_path):
+    # -C: a host chunker cuts each file, sf_index_buffer_blocks hashes its
+    # blocks -- the reference's default mode as a C/Rust caller drops it in
+    exe = _built(False)
+    files = {}
+    for i, n in enumerate([0, 1, 3, 4, 5000, 100_000, (3 << 20) + 11]):
+        data = oracle.splitmix_bytes(n, 900 + i)
+        p = tmp_path / f"c{i}"
+        data.tofile(p)
+        files[str(p)] = data
+    ones = np.full(100_000, 0xFF, np.uint8)  # no trigger at all: 32 KiB blocks
+    zeros = np.zeros(50_000, np.uint8)  # a trigger at every byte from the 4th: 1-byte blocks, the list grows
+    for nm, data in (("ones", ones), ("zeros", zeros)):
+        data.tofile(tmp_path / nm)
+        files[str(tmp_path / nm)] = data
+    r = subprocess.run([exe, "-C"] + list(files), capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    got = _parse(r.stdout.decode())
+    for name, data in files.items():
+        offs, sizes = _cdc_cuts(data)
+        dig = oracle.index_blocks(data, np.asarray(offs, np.uint64), np.asarray(sizes, np.uint32))
+        rows = [(o, s, bytes(d).hex()) for o, s, d in zip(offs, sizes, dig)]
+        assert got[name]["rows"] == rows and got[name]["bh"] == oracle.blocks_hash(dig).hex(), name
+    assert [r[1] for r in got[str(tmp_path / "ones")]["rows"]] == [32768, 32768, 32768, 100_000 - 3 * 32768]
+    assert len(got[str(tmp_path / "zeros")]["rows"]) == 50_000 - 3
