@@ -6,7 +6,7 @@ The list is what the reference's default chunker produces in shape
 (src/index.rs:40-41: ZPAQ 13 bits = 8 KiB mean, 32 KiB cap): geometric sizes,
 mean 8 KiB, capped at 32 KiB, tiling the buffer.  Best of REPS calls each;
 a sample of digests is checked with hashlib.
-Usage: python scripts/buffer_blocks_probe.py [GiB]"""
+Usage: python scripts/buffer_blocks_probe.py [GiB ...]"""
 import hashlib
 import json
 import os
@@ -22,7 +22,11 @@ GiB = 1 << 30
 
 
 def main():
-    gib = float(sys.argv[1]) if len(sys.argv) > 1 else 4.0
+    for arg in (sys.argv[1:] or ["4"]):
+        one(float(arg))
+
+
+def one(gib):
     reps = int(os.environ.get("REPS", "3"))
     n = int(gib * GiB)
     import torch
