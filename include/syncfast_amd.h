@@ -228,6 +228,16 @@ int sf_index_buffer_blocks(const uint8_t *data, uint64_t len, const uint64_t *of
                            const uint32_t *sizes, uint64_t n_blocks, sf_block_sig *out,
                            uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
 
+/* The same list over a regular file on disk: the caller's chunker streamed
+ * the file once to find the boundaries (cdchunking's stream(file),
+ * src/index.rs:625), and the library reads each ~256 MiB window again with
+ * pread (16 threads) into the pinned stages -- the file is never held whole
+ * in memory.  List checked against the file's size first (SF_ERANGE /
+ * SF_EINVAL as above); SF_EIO if it cannot be opened, is not a regular file
+ * or shrinks while being read.  Rows in list order + blocks_hash; blocking. */
+int sf_index_file_blocks(const char *path, const uint64_t *offsets, const uint32_t *sizes,
+                         uint64_t n_blocks, sf_block_sig *out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
 /* End to end from a file on disk (the reference's input, src/index.rs:615):
  * pread into pinned buffers, overlapped H2D + kernel, D2H.  Writes the
  * rows and the file's blocks_hash.  Blocking.  A path that cannot seek (FIFO,

@@ -38,8 +38,12 @@ def one(gib):
     b = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
     offs, szs = b[:-1], np.diff(b).astype(np.uint32)
     res = {"bytes": n, "blocks": int(offs.size), "mean_block": n / offs.size}
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "sf_bb_probe.bin")
+    data.tofile(path)  # page-cache resident for the file forms
     for name, fn in (("fixed4k", lambda: host.index_buffer(data, 4096)),
-                     ("cdc_list", lambda: host.index_buffer_blocks(data, offs, szs))):
+                     ("cdc_list", lambda: host.index_buffer_blocks(data, offs, szs)),
+                     ("file_fixed4k", lambda: host.index_file(path, 4096)),
+                     ("file_cdc_list", lambda: host.index_file_blocks(path, offs, szs))):
         best = None
         out = None
         for _ in range(reps):
@@ -53,6 +57,7 @@ def one(gib):
             assert bytes(rows["sha1"][i]) == hashlib.sha1(data[o:o + s].tobytes()).digest(), (name, i)
         res[name] = {"s": round(best, 4), "GB/s": round(n / best / 1e9, 2), "GiB/s": round(n / best / GiB, 2)}
         print(name, res[name], flush=True)
+    os.unlink(path)
     print(json.dumps(res))
 
 

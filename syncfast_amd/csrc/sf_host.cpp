@@ -538,8 +538,10 @@ constexpr uint64_t kListStageMaxBlocks = 1ull << 22;  // keeps a stage's list an
 // to HBM, sha1_table_kernel hashes the blocks, the digests come back.  While
 // stage k is copied in, stage k-1 is on the device and stage k-2's rows are
 // written and folded into blocks_hash, in list order.
-static int index_list_pipeline(const uint8_t* data, const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
-                               sf_block_sig* out, uint8_t* blocks_hash) {
+// `fill(dst, w0, w1)` puts bytes [w0, w1) of the input into the pinned stage.
+template <typename FillFn>
+int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* sizes, uint64_t n, sf_block_sig* out,
+                        uint8_t* blocks_hash) {
   const uint64_t target = file_stage_bytes(1);  // ~256 MiB (SF_STREAM_STAGE_MIB test knob)
   std::vector<ListStage> stages;
   uint64_t max_win = 0, max_blocks = 0;
@@ -591,7 +593,7 @@ static int index_list_pipeline(const uint8_t* data, const uint64_t* offsets, con
     if (stage_of[b] >= 0 && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (k-1 comes later in list order)
     const ListStage& s = stages[k];
     const uint64_t nb = s.b1 - s.b0, win = s.w1 - s.w0;
-    par_memcpy(static_cast<uint8_t*>(pin[b]), data + s.w0, win);
+    if ((rc = fill(static_cast<uint8_t*>(pin[b]), s.w0, s.w1)) != SF_OK) break;
     uint64_t* lo = static_cast<uint64_t*>(plist[b]);
     uint32_t* lz = reinterpret_cast<uint32_t*>(lo + nb);
     for (uint64_t i = 0; i < nb; i++) {
@@ -649,7 +651,62 @@ static int sf_index_buffer_blocks_body(const uint8_t* data, uint64_t len, const 
     }
     return SF_OK;
   }
-  return index_list_pipeline(data, offsets, sizes, n, out, blocks_hash);
+  auto fill = [&](uint8_t* dst, uint64_t w0, uint64_t w1) {
+    par_memcpy(dst, data + w0, w1 - w0);
+    return SF_OK;
+  };
+  return index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash);
+}
+
+static int sf_index_file_blocks_body(const char* path, const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                                     sf_block_sig* out, uint8_t* blocks_hash) {
+  if (!path || (n && (!offsets || !sizes || !out))) return SF_EINVAL;
+  struct Fd {  // closed on every return, and if an exception unwinds to guarded()
+    int fd;
+    ~Fd() { if (fd >= 0) close(fd); }
+  } f{open(path, O_RDONLY | O_NONBLOCK)};  // a FIFO is refused below, not waited on
+  const int fd = f.fd;
+  if (fd < 0) return SF_EIO;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;  // the list names file offsets: a seekable file
+  const uint64_t len = (uint64_t)sb.st_size;
+  for (uint64_t i = 0; i < n; i++) {
+    if (offsets[i] > len || sizes[i] > len - offsets[i]) return SF_ERANGE;
+    if (i && offsets[i] < offsets[i - 1]) return SF_EINVAL;
+  }
+  int rc = SF_OK;
+  if (n == 0) {
+    if (blocks_hash) {
+      sf_host_sha1_stream bh;
+      sf_host_sha1_begin(&bh);
+      sf_host_sha1_final(&bh, blocks_hash);
+    }
+  } else {
+    const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
+    // windows are read with pread slices on the reader threads; a short read
+    // (the file shrank after the list was made) is SF_EIO
+    auto fill = [&](uint8_t* dst, uint64_t w0, uint64_t w1) {
+      const uint64_t m = w1 - w0;
+      const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(m, nthreads));
+      const uint64_t nslices = ceil_div(m, slice);
+      std::atomic<uint64_t> next{0};
+      std::atomic<int> frc{SF_OK};
+      run_pool((unsigned)std::min<uint64_t>(nthreads, std::max<uint64_t>(nslices, 1)), [&] {
+        for (uint64_t k; (k = next.fetch_add(1)) < nslices && frc.load() == SF_OK;) {
+          const uint64_t a = k * slice, e = std::min(m, a + slice);
+          for (uint64_t got = a; got < e;) {
+            const ssize_t r = pread(fd, dst + got, e - got, (off_t)(w0 + got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r <= 0) { frc.store(SF_EIO); break; }
+            got += (uint64_t)r;
+          }
+        }
+      });
+      return frc.load();
+    };
+    rc = index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash);
+  }
+  return rc;
 }
 
 static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
@@ -840,6 +897,11 @@ int sf_index_buffer(const uint8_t* data, uint64_t len, uint32_t block_size, sf_b
 int sf_index_buffer_blocks(const uint8_t* data, uint64_t len, const uint64_t* offsets, const uint32_t* sizes,
                            uint64_t n_blocks, sf_block_sig* out, uint8_t blocks_hash[20]) {
   return guarded([&] { return sf_index_buffer_blocks_body(data, len, offsets, sizes, n_blocks, out, blocks_hash); });
+}
+
+int sf_index_file_blocks(const char* path, const uint64_t* offsets, const uint32_t* sizes, uint64_t n_blocks,
+                         sf_block_sig* out, uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_file_blocks_body(path, offsets, sizes, n_blocks, out, blocks_hash); });
 }
 
 int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,

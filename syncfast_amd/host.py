@@ -59,6 +59,24 @@ def index_buffer_blocks(data, offsets, sizes) -> Tuple[np.ndarray, bytes]:
     return out[:n], bytes(bh)
 
 
+def index_file_blocks(path, offsets, sizes) -> Tuple[np.ndarray, bytes]:
+    """As index_buffer_blocks over a regular file on disk, read again window
+    by window with pread (sf_index_file_blocks): the boundaries came from a
+    chunker that streamed the file; the file is never held whole in memory."""
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
+    szs = np.ascontiguousarray(sizes, dtype=np.uint32).reshape(-1)
+    if offs.size != szs.size:
+        raise ValueError("offsets and sizes differ in length")
+    n = offs.size
+    out = np.zeros(max(n, 1), SIG_DTYPE)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_file_blocks(os.fsencode(path), offs.ctypes.data if n else None,
+                                     szs.ctypes.data if n else None, n,
+                                     out.ctypes.data_as(ctypes.POINTER(BlockSig)), bh),
+          f"sf_index_file_blocks({os.fsdecode(path)})")
+    return out[:n], bytes(bh)
+
+
 def release_cache() -> None:
     """Free the streams and buffers the host entry points keep between calls
     (sf_release_host_cache)."""

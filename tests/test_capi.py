@@ -94,6 +94,35 @@ def test_buffer_blocks_validation_without_device():
         host.index_buffer_blocks(data, [0, 95], [10, 10])
 
 
+def test_file_blocks_validation_without_device(tmp_path):
+    """sf_index_file_blocks: a path that does not open or is not a regular
+    file is SF_EIO, a block past the FILE's end SF_ERANGE, offsets going
+    backwards SF_EINVAL -- all before any device call."""
+    L = syncfast_amd.lib()
+    p = tmp_path / "f"
+    p.write_bytes(bytes(range(256)) * 4)
+    out = np.zeros(4, host.SIG_DTYPE)
+    pout = out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig))
+
+    def call(path, offs, sizes):
+        o = np.asarray(offs, np.uint64)
+        s = np.asarray(sizes, np.uint32)
+        return L.sf_index_file_blocks(path, o.ctypes.data, s.ctypes.data, o.size, pout, None)
+
+    assert call(b"/nonexistent/file", [0], [1]) == _lib.SF_EIO
+    assert call(bytes(tmp_path), [0], [1]) == _lib.SF_EIO  # a directory
+    fifo = tmp_path / "fifo"
+    os.mkfifo(fifo)  # no writer: refused at once, not waited on
+    assert call(bytes(fifo), [0], [1]) == _lib.SF_EIO
+    assert call(bytes(p), [0, 1000], [1000, 25]) == _lib.SF_ERANGE  # 1025 > 1024
+    assert call(bytes(p), [10, 5], [1, 1]) == _lib.SF_EINVAL
+    assert L.sf_index_file_blocks(None, None, None, 0, None, None) == _lib.SF_EINVAL
+    rows, bh = host.index_file_blocks(p, [], [])
+    assert rows.size == 0 and bh == hashlib.sha1(b"").digest()
+    with pytest.raises(_lib.SfError, match="nonexistent"):
+        host.index_file_blocks("/nonexistent/file", [0], [1])
+
+
 def test_host_paths_without_device():
     """Without a GPU the host-memory entry points fail cleanly: the in-place
     route (>= 1 MiB) cannot page-lock, the staged route cannot set up its

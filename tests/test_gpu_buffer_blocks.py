@@ -162,3 +162,45 @@ def test_stage_knob_does_not_change_results(gpu):
         del os.environ["SF_STREAM_STAGE_MIB"]
         host.release_cache()
     assert np.array_equal(a[0], b[0]) and a[1] == b[1]
+
+
+def test_file_form_equals_buffer_form(gpu, tmp_path, small_stages):
+    """sf_index_file_blocks preads the windows the buffer form copies: same
+    rows, same blocks_hash, across 1 MiB stages, with a block past 1 MiB."""
+    rng = np.random.default_rng(21)
+    n = (5 << 20) + 321
+    data = oracle.splitmix_bytes(n, 21)
+    p = tmp_path / "cdc.bin"
+    data.tofile(p)
+    offs, sizes = _cdc_like(rng, n)
+    a = host.index_file_blocks(p, offs, sizes)
+    b = host.index_buffer_blocks(data, offs, sizes)
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1]
+    _check(data, offs, sizes)
+    big_offs = [0, 100, 100 + (3 << 20)]
+    big_sizes = [100, 3 << 20, n - 100 - (3 << 20)]
+    c = host.index_file_blocks(p, big_offs, big_sizes)
+    d = _check(data, big_offs, big_sizes)
+    assert np.array_equal(c[0], d)
+
+
+def test_file_form_reference_kat(gpu, tmp_path):
+    p = tmp_path / "kat"
+    p.write_bytes(oracle.kat_input())
+    rows, bh = host.index_file_blocks(p, KAT_OFFS, KAT_SIZES)
+    assert [bytes(r).hex() for r in rows["sha1"]] == KAT_DIGESTS
+    assert bh.hex() == KAT_BLOCKS_HASH
+
+
+def test_file_form_errors(gpu, tmp_path):
+    from syncfast_amd._lib import SF_EIO, SF_ERANGE, SfError
+    p = tmp_path / "short"
+    p.write_bytes(b"x" * 5000)
+    with pytest.raises(SfError) as e:
+        host.index_file_blocks(p, [0, 4000], [4000, 1001])
+    assert e.value.errno == -SF_ERANGE
+    fifo = tmp_path / "fifo"
+    os.mkfifo(fifo)  # no writer: the library must not wait for one
+    with pytest.raises(SfError) as e:
+        host.index_file_blocks(fifo, [0], [1])
+    assert e.value.errno == -SF_EIO
