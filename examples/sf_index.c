@@ -13,7 +13,8 @@
  *   ./sf_index [-b block_size] [-m | -B | -s N] path...
  *     -m: all paths through one sf_index_files call; -B: each file from a host
  *     buffer (sf_index_buffer); -C: each file cut by a content-defined chunker
- *     on the host, its blocks hashed by sf_index_buffer_blocks;
+ *     on the host, its blocks hashed by sf_index_buffer_blocks (and again by
+ *     sf_index_file_blocks, which must agree);
  *     -s N: each file as N sf_index_file_range shards;
  *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
  *     -L dst src: src's blocks looked up among dst's (sf_block_set_*)
@@ -166,6 +167,14 @@ static int index_cdc(const char *path) {
     }
     if (rc == SF_OK) rc = (rows = malloc((n ? n : 1) * sizeof(sf_block_sig))) ? SF_OK : SF_ENOMEM;
     if (rc == SF_OK) rc = sf_index_buffer_blocks(buf, len, offs, sizes, n, rows, bh);
+    if (rc == SF_OK) {  /* the file form (pread windows) must give the same rows and blocks_hash */
+        sf_block_sig *again = malloc((n ? n : 1) * sizeof(sf_block_sig));
+        uint8_t bh2[20];
+        rc = again ? sf_index_file_blocks(path, offs, sizes, n, again, bh2) : SF_ENOMEM;
+        if (rc == SF_OK && (memcmp(bh, bh2, 20) != 0 || (n && memcmp(rows, again, n * sizeof(sf_block_sig)) != 0)))
+            rc = SF_EIO;
+        free(again);
+    }
     if (rc == SF_OK) print_rows(path, rows, n, bh);
     free(buf);
     free(offs);

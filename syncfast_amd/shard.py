@@ -46,6 +46,31 @@ def shard_blocks(total_len: int, block_size: int, world: int) -> List[int]:
     return out
 
 
+def list_shards(offsets, sizes, world: int) -> List[int]:
+    """Block-index cuts [c_0 = 0, c_1, ..., c_world = n] of an offset-ordered
+    block list (a chunker's output): rank r takes blocks [c_r, c_{r+1}), the
+    first block starting at or after r/world of the list's byte span, so
+    the ranks' byte shares are about even (to within one block for a
+    tiling list).  Content-defined
+    boundaries need no fix-up between ranks here: the host chunker cut the
+    whole file before the list was split."""
+    import numpy as np
+    offs = np.asarray(offsets, dtype=np.uint64).reshape(-1)
+    n = offs.size
+    if world < 1:
+        raise ValueError("bad world")
+    if n == 0:
+        return [0] * (world + 1)
+    lo = int(offs[0])
+    hi = int((offs + np.asarray(sizes, dtype=np.uint64).reshape(-1)).max())
+    cuts = [0]
+    for r in range(1, world):
+        target = lo + (hi - lo) * r // world
+        cuts.append(max(cuts[-1], int(np.searchsorted(offs, np.uint64(target), side="left"))))
+    cuts.append(n)
+    return cuts
+
+
 def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
                    group: Optional[dist.ProcessGroup] = None, dst: int = 0,
                    async_op: bool = False):
@@ -56,10 +81,19 @@ def gather_digests(local: torch.Tensor, total_len: int, block_size: int,
     Returns the full uint8[n, 20] table on `dst` (None elsewhere); with
     async_op, returns (work, finish) where finish() -> table after
     work.wait()."""
+    counts = shard_blocks(total_len, block_size, dist.get_world_size(group))
+    return gather_digests_counts(local, counts, group, dst, async_op)
+
+
+def gather_digests_counts(local: torch.Tensor, counts: List[int], group: Optional[dist.ProcessGroup] = None,
+                          dst: int = 0, async_op: bool = False):
+    """gather_digests with every rank's row count given (an explicit block
+    list's shards, list_shards)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)  # shard index: the rank within `group`
     is_dst = dist.get_rank() == dst  # `dst` is a global rank, as dist.gather takes it
-    counts = shard_blocks(total_len, block_size, world)
+    if len(counts) != world:
+        raise ValueError("one count per rank")
     if local.shape[0] != counts[rank]:
         raise ValueError(f"rank {rank} holds {local.shape[0]} digests, shard has {counts[rank]}")
     m = max(counts) if counts else 0
@@ -139,5 +173,55 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
     out["size"] = block_size
     if n:
         out["size"][-1] = size - (n - 1) * block_size
+    out["sha1"] = table
+    return out, host.blocks_hash(table)
+
+
+def index_file_blocks_sharded(path, offsets, sizes, group: Optional[dist.ProcessGroup] = None, dst: int = 0,
+                              device: Optional[torch.device] = None):
+    """The reference's default (content-defined) blocks of one file on N
+    ranks: every rank holds the same offset-ordered list (the host chunker's
+    output over the file, src/index.rs:622-625), takes its list_shards range
+    and hashes those blocks from the file on its own GPU
+    (sf_index_file_blocks); the digests are gathered to `dst`, which returns
+    the file's rows in list order and its blocks_hash (src/index.rs:661-682).
+    The ranks agree on success before the gather, as index_file_sharded does.
+    Returns (rows, blocks_hash) on `dst`, None elsewhere."""
+    import os
+
+    import numpy as np
+
+    from . import host
+    from ._lib import SF_EIO, SfError
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    is_dst = dist.get_rank() == dst
+    where = device if device is not None else torch.device("cpu")
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
+    szs = np.ascontiguousarray(sizes, dtype=np.uint32).reshape(-1)
+    cuts = list_shards(offs, szs, world)
+    b0, b1 = cuts[rank], cuts[rank + 1]
+    failure: Optional[BaseException] = None
+    try:
+        rows, _ = host.index_file_blocks(path, offs[b0:b1], szs[b0:b1])
+    except (SfError, OSError, ValueError) as e:
+        failure = e
+    failed = torch.tensor([1 if failure is not None else 0], dtype=torch.int32, device=where)
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=group)
+    if failure is not None:
+        raise failure
+    if int(failed.item()):
+        raise SfError(SF_EIO, f"index_file_blocks_sharded: another rank failed on {os.fsdecode(path)}")
+    dig = torch.from_numpy(np.ascontiguousarray(rows["sha1"]).reshape(-1, 20))
+    if device is not None:
+        dig = dig.to(device)
+    counts = [cuts[r + 1] - cuts[r] for r in range(world)]
+    table = gather_digests_counts(dig, counts, group=group, dst=dst)
+    if not is_dst:
+        return None
+    table = table.cpu().numpy()
+    out = np.zeros(offs.size, host.SIG_DTYPE)
+    out["offset"] = offs
+    out["size"] = szs
     out["sha1"] = table
     return out, host.blocks_hash(table)

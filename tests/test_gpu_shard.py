@@ -197,3 +197,57 @@ def test_rccl_gather_path_world1(gpu):
     assert p.exitcode == 0 and ok
     n, bs = (16 << 20) + 5, 4096
     assert got == oracle.index_fixed(oracle.splitmix_bytes(n, 0x5EED0008), bs)[2].tobytes()
+
+
+def _list_rank(rank, world, port, path, offs, sizes, q):
+    import torch.distributed as dist
+
+    from syncfast_amd.shard import index_file_blocks_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = index_file_blocks_sharded(path, offs, sizes)
+        if rank == 0:
+            rows, bh = res
+            q.put((rows.tobytes(), bh))
+        else:
+            assert res is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hip_list_shards_gathered_equal_whole_list(gpu, tmp_path, world):
+    """The default (content-defined) mode on N ranks: the host chunker's list
+    split by list_shards, each rank hashing its blocks from the file through
+    the HIP path (sf_index_file_blocks), gathered to rank 0 = the whole list's
+    rows and blocks_hash (oracle)."""
+    import torch.multiprocessing as mp
+
+    from syncfast_amd import host
+    rng = np.random.default_rng(world)
+    n = (24 << 20) + 999
+    data = oracle.splitmix_bytes(n, 0x5EED0200)
+    path = tmp_path / "cdc.bin"
+    data.tofile(path)
+    sizes = np.minimum(rng.geometric(1 / 8192, n // 2000), 32768).astype(np.uint64)
+    cuts = np.cumsum(sizes)
+    cuts = cuts[cuts < n]
+    b = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+    offs, szs = b[:-1], np.diff(b).astype(np.uint32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_list_rank, args=(r, world, port, str(path), offs, szs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rows_b, bh = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rows = np.frombuffer(rows_b, host.SIG_DTYPE)
+    want = oracle.index_blocks(data, offs, szs)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], szs)
+    assert np.array_equal(rows["sha1"], want)
+    assert bh == oracle.blocks_hash(want)

@@ -205,3 +205,63 @@ def test_index_file_sharded_subgroup_global_dst(tmp_path):
     offs, sizes, want = oracle.index_fixed(data, bs)
     assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
     assert np.array_equal(rows["sha1"], want) and got[2][1] == oracle.blocks_hash(want)
+
+
+def test_list_shards_partition_a_block_list():
+    from syncfast_amd.shard import list_shards
+    rng = np.random.default_rng(4)
+    for n_blocks, world in [(0, 3), (1, 4), (10, 2), (5000, 8), (777, 3)]:
+        sizes = np.minimum(rng.geometric(1 / 8192, n_blocks), 32768).astype(np.uint64)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) if n_blocks else np.zeros(0, np.uint64)
+        cuts = list_shards(offs, sizes, world)
+        assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == n_blocks
+        assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+        if n_blocks > 100 * world:  # tiling list: every rank's bytes within one block (32 KiB) of an even share
+            total = int(sizes.sum())
+            for r in range(world):
+                share = int(sizes[cuts[r]:cuts[r + 1]].sum())
+                assert abs(share - total / world) <= 2 * 32768
+
+
+def _list_worker(rank, world, port, data, offs, sizes, q):
+    from syncfast_amd.shard import gather_digests_counts, list_shards
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cuts = list_shards(offs, sizes, world)
+        mine = oracle.index_blocks(data, offs[cuts[rank]:cuts[rank + 1]], sizes[cuts[rank]:cuts[rank + 1]])
+        counts = [cuts[r + 1] - cuts[r] for r in range(world)]
+        full = gather_digests_counts(torch.from_numpy(mine), counts)
+        if rank == 0:
+            q.put(full.numpy().tobytes())
+        else:
+            assert full is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_of_list_shards_is_the_list_table(world):
+    """An explicit (content-defined-like) list split by list_shards, each
+    rank's digests gathered with uneven counts: rank 0 holds the list's table
+    in list order (digests by the oracle here: no GPU on this machine)."""
+    rng = np.random.default_rng(world)
+    n = 600_000
+    data = oracle.splitmix_bytes(n, 0x5EED0100)
+    sizes = np.minimum(rng.geometric(1 / 8192, n // 1000), 32768).astype(np.uint64)
+    cuts = np.cumsum(sizes)
+    cuts = cuts[cuts < n]
+    b = np.concatenate([[0], cuts, [n]]).astype(np.uint64)
+    offs, szs = b[:-1], np.diff(b).astype(np.uint32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_list_worker, args=(r, world, port, data, offs, szs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == oracle.index_blocks(data, offs, szs).tobytes()
