@@ -442,10 +442,15 @@ class Index:
         self._index_path_rec(Path(path), PurePath(""), todo)
         if not todo:
             return
-        if not isinstance(self.chunker, FixedChunker) or batch_bytes <= 0:
+        if batch_bytes <= 0:
             for p, rel in todo:
                 self.index_file(p, rel)
             return
+        if isinstance(self.chunker, BoundaryChunker):
+            self._index_batched_boundaries(todo, batch_bytes)
+            return
+        if not isinstance(self.chunker, FixedChunker):
+            raise TypeError("unknown chunker")
         self._index_batched(todo, batch_bytes)
 
     def _index_path_rec(self, root: Path, rel: PurePath, todo) -> None:
@@ -491,6 +496,59 @@ class Index:
         for k, (file_id, _p) in enumerate(pending):
             self._insert_rows(file_id, rows, int(first[k]), int(first[k + 1]))
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
+
+    def _index_batched_boundaries(self, todo, batch_bytes: int) -> None:
+        """The default (content-defined) mode over many files: each file is
+        read and cut by the host chunker, and the blocks of up to
+        `batch_bytes` of files go to the device in ONE sf_index_buffer_blocks
+        call (their bytes back to back, one offset-ordered list), so the
+        per-call latency of a long block's chain is paid
+        per batch, not per file.  Rows get file offsets back; each file's
+        blocks_hash is the SHA-1 over its digests in offset order, the value
+        compute_blocks_hash reads back (src/index.rs:661-682)."""
+        batch = []  # (file_id, base, n_bytes, sizes)
+        parts: List[bytes] = []
+        nbytes = 0
+
+        def flush():
+            nonlocal batch, parts, nbytes
+            if not batch:
+                return
+            offs = np.zeros(sum(len(sz) for _f, _b, _n, sz in batch), np.uint64)
+            sizes = np.zeros(offs.size, np.uint32)
+            k = 0
+            for _fid, base, _n, sz in batch:
+                if sz:
+                    a = np.asarray(sz, np.uint64)
+                    offs[k:k + a.size] = base + np.concatenate([[0], np.cumsum(a)[:-1]]).astype(np.uint64)
+                    sizes[k:k + a.size] = a
+                    k += a.size
+            rows, _ = host.index_buffer_blocks(b"".join(parts), offs, sizes)
+            k = 0
+            for fid, base, _n, sz in batch:
+                mine = rows[k:k + len(sz)].copy()
+                k += len(sz)
+                mine["offset"] -= np.uint64(base)
+                self._insert_rows(fid, mine)
+                bh = host.blocks_hash(np.ascontiguousarray(mine["sha1"]))
+                self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.hex(), fid))
+            batch, parts, nbytes = [], [], 0
+
+        for p, rel in todo:
+            with open(p, "rb") as f:  # File::open first: same error on a missing file
+                file_id, up_to_date = self.add_file(rel, _mtime(f))
+                if up_to_date:
+                    continue
+                raw = f.read()  # a FIFO in the tree is read from this open, to EOF
+            sizes = [int(x) for x in self.chunker.fn(raw)]
+            if any(x <= 0 for x in sizes) or sum(sizes) != len(raw):
+                raise ValueError("boundary function must return positive sizes covering the data")
+            batch.append((file_id, nbytes, len(raw), sizes))
+            parts.append(raw)
+            nbytes += len(raw)
+            if nbytes >= batch_bytes:
+                flush()
+        flush()
 
     def remove_missing_files(self, path) -> None:
         """src/index.rs:718-726."""

@@ -185,6 +185,53 @@ def test_index_path_fixed_blocks(gpu, tmp_path, batch_bytes):
     assert "sub/b.bin" not in {str(f[1]) for f in idx.list_files()}
 
 
+def _toy_cdc(data: bytes):
+    """A content-defined boundary function for the tests (a stand-in for the
+    reference's ZPAQ): cut after every byte 0x00 that follows 7 or more bytes
+    since the last cut, or at 2000 bytes."""
+    sizes, start = [], 0
+    for i, c in enumerate(data):
+        if (c == 0 and i + 1 - start >= 8) or i + 1 - start == 2000:
+            sizes.append(i + 1 - start)
+            start = i + 1
+    if start < len(data):
+        sizes.append(len(data) - start)
+    return sizes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch_bytes", [0, 1 << 30, 30_000])
+def test_index_path_boundary_chunker_batched(gpu, tmp_path, batch_bytes):
+    """index_path in the default (content-defined) mode: files cut by the host
+    chunker, their blocks hashed per batch of files in one device call; the
+    rows, the stored blocks_hash and its SELECT recomputation equal the
+    per-file path and the oracle."""
+    root = tmp_path / "tree"
+    (root / "sub").mkdir(parents=True)
+    files = {"a.bin": 100_000, "sub/b.bin": 12_345, "sub/empty": 0, "c": 1, "d": 7_777}
+    for i, (n, ln) in enumerate(files.items()):
+        (root / n).write_bytes(oracle.splitmix_bytes(ln, 3000 + i).tobytes())
+    idx = Index.open(root / ".syncfast.idx", chunker=BoundaryChunker(_toy_cdc))
+    idx.index_path(root, batch_bytes=batch_bytes)
+    idx.commit()
+    assert {str(f[1]) for f in idx.list_files()} == set(files)
+    for i, (n, ln) in enumerate(files.items()):
+        fid, _, bh = idx.get_file(n)
+        data = oracle.splitmix_bytes(ln, 3000 + i).tobytes()
+        sizes = _toy_cdc(data)
+        offs = [sum(sizes[:k]) for k in range(len(sizes))]
+        want = oracle.py_index_blocks(data, offs, sizes)
+        got = idx.list_file_blocks(fid)
+        assert [(g[0].bytes, g[1], g[2]) for g in got] == list(zip(want, offs, sizes)), n
+        assert bh.bytes == oracle.py_blocks_hash(want)
+        assert idx.compute_blocks_hash(fid) == bh
+    # unchanged mtimes: nothing re-indexed
+    before = idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0]
+    idx.index_path(root, batch_bytes=batch_bytes)
+    idx.commit()
+    assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("via", ["index_file", "index_path"])
 def test_fifo_is_streamed(gpu, tmp_path, via):
