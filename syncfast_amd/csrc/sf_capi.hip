@@ -514,7 +514,11 @@ int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t
   // waves per workgroup for the rest
   const uint64_t C_ = cj[0].waves + cj[1].waves;
   const uint64_t bwaves = ceil_div(total, 64);
+#if defined(SF_TUNING) && defined(SF_CHAIN_SOLO)
+  const uint64_t rest = bwaves;  // A/B only: chain workgroups hold the chain wave alone
+#else
   const uint64_t rest = bwaves > 3 * C_ ? bwaves - 3 * C_ : 0;
+#endif
   const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
   if (grid == 0) return SF_OK;
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),

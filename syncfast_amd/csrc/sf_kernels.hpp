@@ -658,10 +658,17 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
       else chain_job(j1, g - j0.waves);
       return;
     }
+#if defined(SF_TUNING) && defined(SF_CHAIN_SOLO)
+    return;  // A/B only: the chain wave's workgroup hashes no blocks
+  } else {
+    bw = (uint64_t)(g - C) * kWavesPerWG + wid;
+  }
+#else
     bw = (uint64_t)g * 3 + (wid - 1);
   } else {
     bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
   }
+#endif
   fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, bw, smem + wid * 64 * (TILE / 16));
 }
 
