@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -539,9 +540,14 @@ constexpr uint64_t kListStageMaxBlocks = 1ull << 22;  // keeps a stage's list an
 // stage k is copied in, stage k-1 is on the device and stage k-2's rows are
 // written and folded into blocks_hash, in list order.
 // `fill(dst, w0, w1)` puts bytes [w0, w1) of the input into the pinned stage.
+// `direct` (the buffer form): the caller's bytes, copied to HBM in place --
+// page-locked region by region one stage ahead, as index_inplace does -- when
+// the stage windows are disjoint and at least two pages each (a chunker's
+// list); a region that cannot be page-locked sends it and every later stage
+// through `fill`.
 template <typename FillFn>
 int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* sizes, uint64_t n, sf_block_sig* out,
-                        uint8_t* blocks_hash) {
+                        uint8_t* blocks_hash, const uint8_t* direct = nullptr) {
   const uint64_t target = file_stage_bytes(1);  // ~256 MiB (SF_STREAM_STAGE_MIB test knob)
   std::vector<ListStage> stages;
   uint64_t max_win = 0, max_blocks = 0;
@@ -557,6 +563,44 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
     max_blocks = std::max(max_blocks, s.b1 - s.b0);
     stages.push_back(s);
   }
+  // In-place regions: region k = [edge(k), edge(k+1)), edge(k) = the page
+  // edge at or above stage k's window start (edge(0) below it), so stage k's
+  // bytes lie in region k-1 (its head, up to edge(k)) and region k.
+  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+  const size_t nst = stages.size();
+  bool inplace = direct != nullptr;
+  if (inplace) {
+    const char* noreg = getenv("SF_NO_HOSTREG");
+    inplace = !(noreg && atoi(noreg)) && stages.back().w1 - stages[0].w0 >= inplace_min_bytes(false);
+    for (size_t k = 0; k < nst && inplace; k++)
+      inplace = stages[k].w1 - stages[k].w0 >= 2 * pg && (k == 0 || stages[k - 1].w1 <= stages[k].w0);
+  }
+  auto edge = [&](size_t k) -> uintptr_t {
+    const uintptr_t up = ~(uintptr_t)(pg - 1);
+    if (k == 0) return (uintptr_t)(direct + stages[0].w0) & up;
+    if (k >= nst) return ((uintptr_t)(direct + stages[nst - 1].w1) + pg - 1) & up;
+    return ((uintptr_t)(direct + stages[k].w0) + pg - 1) & up;
+  };
+  enum { kLocked, kPinned, kFailed };
+  std::vector<int> region;  // state of region k
+  struct Unreg {  // declared before the lease: the lease's release syncs the streams first
+    std::vector<int>* r;
+    std::function<uintptr_t(size_t)> e;
+    ~Unreg() {
+      for (size_t k = 0; k < r->size(); k++)
+        if ((*r)[k] == kLocked) (void)hipHostUnregister((void*)e(k));
+    }
+  } unreg{&region, edge};
+  const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to page-lock
+  const long fail_k = fail_at ? atol(fail_at) : -1;
+  auto lock_region = [&](size_t k) {
+    if ((!region.empty() && region.back() == kFailed) || (long)k == fail_k) { region.push_back(kFailed); return; }
+    const uintptr_t a = edge(k), e = edge(k + 1);
+    const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
+    if (err != hipSuccess) (void)hipGetLastError();
+    region.push_back(err == hipSuccess ? kLocked : err == hipErrorHostMemoryAlreadyRegistered ? kPinned : kFailed);
+  };
+  if (inplace) lock_region(0);
   HostLease res;
   hipStream_t* st;
   hipEvent_t* done;
@@ -593,7 +637,8 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
     if (stage_of[b] >= 0 && (rc = harvest(b)) != SF_OK) break;  // stage k-2 (k-1 comes later in list order)
     const ListStage& s = stages[k];
     const uint64_t nb = s.b1 - s.b0, win = s.w1 - s.w0;
-    if ((rc = fill(static_cast<uint8_t*>(pin[b]), s.w0, s.w1)) != SF_OK) break;
+    const bool direct_k = inplace && region[k] != kFailed && (k == 0 || region[k - 1] != kFailed);
+    if (!direct_k && (rc = fill(static_cast<uint8_t*>(pin[b]), s.w0, s.w1)) != SF_OK) break;
     uint64_t* lo = static_cast<uint64_t*>(plist[b]);
     uint32_t* lz = reinterpret_cast<uint32_t*>(lo + nb);
     for (uint64_t i = 0; i < nb; i++) {
@@ -602,12 +647,22 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
     }
     const uint64_t* d_off = static_cast<const uint64_t*>(dlist[b]);
     const uint32_t* d_sz = reinterpret_cast<const uint32_t*>(d_off + nb);
-    if ((win && hipMemcpyAsync(ddata[b], pin[b], win, hipMemcpyHostToDevice, st[b]) != hipSuccess) ||
-        hipMemcpyAsync(dlist[b], plist[b], nb * (sizeof(uint64_t) + sizeof(uint32_t)), hipMemcpyHostToDevice,
-                       st[b]) != hipSuccess) {
+    bool copy_ok = true;
+    if (direct_k) {  // a copy lies inside ONE registration: the head (region k-1) apart from the rest
+      const uint8_t* src = direct + s.w0;
+      const uint64_t head = k == 0 ? 0 : std::min<uint64_t>(win, edge(k) - (uintptr_t)src);
+      copy_ok = (!head || hipMemcpyAsync(ddata[b], src, head, hipMemcpyHostToDevice, st[b]) == hipSuccess) &&
+                (win == head || hipMemcpyAsync(static_cast<uint8_t*>(ddata[b]) + head, src + head, win - head,
+                                               hipMemcpyHostToDevice, st[b]) == hipSuccess);
+    } else if (win) {
+      copy_ok = hipMemcpyAsync(ddata[b], pin[b], win, hipMemcpyHostToDevice, st[b]) == hipSuccess;
+    }
+    if (!copy_ok || hipMemcpyAsync(dlist[b], plist[b], nb * (sizeof(uint64_t) + sizeof(uint32_t)),
+                                   hipMemcpyHostToDevice, st[b]) != hipSuccess) {
       rc = SF_ENODEV;
       break;
     }
+    if (inplace && k + 1 < nst) lock_region(k + 1);  // one region ahead of the copies that read it
     // every block was checked to lie in [0, len), so in its window: no status word
     if ((rc = launch_table(ddata[b], win, d_off, d_sz, nb, ddig[b], nullptr, st[b])) != SF_OK) break;
     if (hipMemcpyAsync(pdig[b], ddig[b], nb * 20, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
@@ -655,7 +710,7 @@ static int sf_index_buffer_blocks_body(const uint8_t* data, uint64_t len, const 
     par_memcpy(dst, data + w0, w1 - w0);
     return SF_OK;
   };
-  return index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash);
+  return index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash, data);
 }
 
 static int sf_index_file_blocks_body(const char* path, const uint64_t* offsets, const uint32_t* sizes, uint64_t n,

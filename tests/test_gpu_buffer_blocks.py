@@ -204,3 +204,22 @@ def test_file_form_errors(gpu, tmp_path):
     with pytest.raises(SfError) as e:
         host.index_file_blocks(fifo, [0], [1])
     assert e.value.errno == -SF_EIO
+
+
+@pytest.mark.parametrize("env", [{}, {"SF_NO_HOSTREG": "1"}, {"SF_INPLACE_FAIL_AT": "0"},
+                                 {"SF_INPLACE_FAIL_AT": "2"}])
+def test_in_place_and_staged_routes_agree(gpu, monkeypatch, env):
+    """The buffer form copies a chunker's list in place (page-locked region by
+    region) or through the pinned stages (SF_NO_HOSTREG=1, overlapping
+    windows, or a region that cannot be page-locked -- SF_INPLACE_FAIL_AT=k
+    from region k on); every route gives the oracle's rows and blocks_hash."""
+    monkeypatch.setenv("SF_STREAM_STAGE_MIB", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(33)
+    n = (6 << 20) + 4321
+    raw = oracle.splitmix_bytes(n + 5, 33)
+    for data in (raw[:n], raw[5:]):  # page-aligned-ish and odd start
+        offs, sizes = _cdc_like(rng, n)
+        _check(data, offs, sizes)
+    host.release_cache()
