@@ -96,6 +96,9 @@ def parse():
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the end-to-end leg (the same bytes from a host buffer through sf_index_buffer)")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--gather-root", default="rotate", choices=("rotate", "fixed"),
+                   help="rank that receives each step's tables: rotates over the ranks, the last step's being "
+                        "rank 0 (files owned round-robin, as a multi-file indexer spreads them), or always 0")
     p.add_argument("--c3-mode", default="stream", choices=("stream", "staged"),
                    help="config 3: 'stream' = batch after batch, each launch also finishing the previous batch's "
                         "blocks_hash (sf_index_device_batch_chained); 'staged' = one self-contained launch per batch")
@@ -337,10 +340,21 @@ def main():
     last_table = [None]
     last_hashes = [None]  # batch stream: blocks_hash of the latest finished batch
 
+    def root(i, timed):
+        # The rank that receives step i's tables (the owner of that step's
+        # logical file: it writes the rows and computes blocks_hash).  With a
+        # fixed root that rank takes (N-1) tables every step and runs ~3.7 %
+        # behind the others (scripts/gather_sim.py), which the max-over-ranks
+        # clock charges to the whole job; rotating spreads the receive load,
+        # and the last timed step's root is rank 0, which checks its table.
+        if a.gather_root == "fixed":
+            return 0
+        return ((i - (a.steps - 1)) if timed else i) % world
+
     def step(i, timed):
         b = i % nbuf
         if pending[b] is not None:  # the gather that reads digs[b] must be done
-            work, finish = pending[b]
+            work, finish, _ = pending[b]
             work.wait()
             last_table[0] = finish  # concatenated only once, after the timed loop
             pending[b] = None
@@ -360,15 +374,15 @@ def main():
         if timed:
             ev[i][1].record(stream)
         if gather:
-            pending[b] = gather_digests(digs[b], total, bs, async_op=True)
+            pending[b] = gather_digests(digs[b], total, bs, dst=root(i, timed), async_op=True) + (i,)
 
     def drain():
-        for b in range(nbuf):
-            if pending[b] is not None:
-                work, finish = pending[b]
-                work.wait()
-                last_table[0] = finish
-                pending[b] = None
+        # in step order, so last_table ends as the last step's gather (rank 0's)
+        for b in sorted((b for b in range(nbuf) if pending[b] is not None), key=lambda b: pending[b][2]):
+            work, finish, _ = pending[b]
+            work.wait()
+            last_table[0] = finish
+            pending[b] = None
 
     # Setup (not a step): clock ramp, untimed, no gather.
     t_ramp = time.perf_counter()
@@ -430,6 +444,8 @@ def main():
             dist.destroy_process_group()
         return
 
+    if gather and gathered is None:
+        raise SystemExit("rank 0 received no table from the last step's gather")
     if gathered is not None:  # rank 0 owns the whole file's table, rank order
         assert gathered.shape[0] == total // bs and torch.equal(gathered[:nblk].to(dig.device), dig)
 
@@ -494,7 +510,9 @@ def main():
                    "total_bytes": total_bytes, "files": cfg["files"], "blocks": nblk * world,
                    **({"c3_mode": a.c3_mode} if files else {}),
                    "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else a.dist_backend}"
-                                                     "_gather(pipelined)" if gather else "")},
+                                                     "_gather(pipelined, root %s)" % (
+                                                         "rotating" if a.gather_root == "rotate" else "0")
+                                                     if gather else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": ("sha1_fixed_chained_kernel<128>" if bstream is not None else
