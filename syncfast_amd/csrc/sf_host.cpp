@@ -32,6 +32,49 @@ using namespace sfi;
 
 namespace {
 
+// Host ranges page-locked by this library's in-place routes, process-wide.
+// hipHostRegister refuses a range that overlaps a registered one
+// (AlreadyRegistered).  If that registration is one of ours, the concurrent
+// call that made it will unregister it while our copies may still read it,
+// so such a range is bounced through pinned stages instead; a registration
+// the caller made stays for the length of the call and is copied from.
+enum PageLock { kLockedByUs, kPinnedByCaller, kNotLocked };
+std::mutex g_lock_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_locked;
+
+bool locked_by_us(uintptr_t a, uintptr_t e) {  // caller holds g_lock_mu
+  for (const auto& r : g_locked)
+    if (r.first < e && a < r.second) return true;
+  return false;
+}
+
+PageLock lock_pages(uintptr_t a, uintptr_t e) {
+  std::lock_guard<std::mutex> lk(g_lock_mu);
+  if (locked_by_us(a, e)) return kNotLocked;
+  const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
+  if (err == hipSuccess) {
+    g_locked.push_back({a, e});
+    return kLockedByUs;
+  }
+  (void)hipGetLastError();
+  return err == hipErrorHostMemoryAlreadyRegistered ? kPinnedByCaller : kNotLocked;
+}
+
+void unlock_pages(uintptr_t a) {
+  std::lock_guard<std::mutex> lk(g_lock_mu);
+  (void)hipHostUnregister((void*)a);
+  for (size_t i = 0; i < g_locked.size(); i++)
+    if (g_locked[i].first == a) {
+      g_locked.erase(g_locked.begin() + (long)i);
+      break;
+    }
+}
+
+bool range_locked_by_us(uintptr_t a, uintptr_t e) {
+  std::lock_guard<std::mutex> lk(g_lock_mu);
+  return locked_by_us(a, e);
+}
+
 // RAII pinned allocation (the in-place route's bounce buffer).
 struct PinBuf {
   void* p = nullptr;
@@ -107,7 +150,7 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
     std::vector<std::pair<void*, int>>* r;
     ~Unreg() {
       for (auto& x : *r)
-        if (x.second == kLocked) (void)hipHostUnregister(x.first);
+        if (x.second == kLocked) unlock_pages((uintptr_t)x.first);
     }
   } unreg{&regs};
   // A buffer that is already page-locked (hipHostMalloc, or registered by the
@@ -120,7 +163,8 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
     }
     return at.type == hipMemoryTypeHost;
   };
-  const bool prepinned = pinned_at(data) && pinned_at(data + len - 1);
+  // (pages a concurrent call of ours locked are not the caller's pinning)
+  const bool prepinned = pinned_at(data) && pinned_at(data + len - 1) && !range_locked_by_us(lo, hi);
   const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to register
   const long fail_k = fail_at ? atol(fail_at) : -1;
   auto reg = [&](uint64_t k) {
@@ -133,11 +177,8 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
       regs.push_back({(void*)a, kPageable});
       return;
     }
-    const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
-    if (err != hipSuccess) (void)hipGetLastError();
-    regs.push_back({(void*)a, err == hipSuccess                               ? kLocked
-                              : err == hipErrorHostMemoryAlreadyRegistered ? kPinned
-                                                                           : kPageable});
+    const PageLock pl = lock_pages(a, e);
+    regs.push_back({(void*)a, pl == kLockedByUs ? kLocked : pl == kPinnedByCaller ? kPinned : kPageable});
   };
   reg(0);
   if (regs[0].second != kLocked && regs[0].second != kPinned) return SF_ENOTSUP;
@@ -588,17 +629,15 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
     std::function<uintptr_t(size_t)> e;
     ~Unreg() {
       for (size_t k = 0; k < r->size(); k++)
-        if ((*r)[k] == kLocked) (void)hipHostUnregister((void*)e(k));
+        if ((*r)[k] == kLocked) unlock_pages(e(k));
     }
   } unreg{&region, edge};
   const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to page-lock
   const long fail_k = fail_at ? atol(fail_at) : -1;
   auto lock_region = [&](size_t k) {
     if ((!region.empty() && region.back() == kFailed) || (long)k == fail_k) { region.push_back(kFailed); return; }
-    const uintptr_t a = edge(k), e = edge(k + 1);
-    const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
-    if (err != hipSuccess) (void)hipGetLastError();
-    region.push_back(err == hipSuccess ? kLocked : err == hipErrorHostMemoryAlreadyRegistered ? kPinned : kFailed);
+    const PageLock pl = lock_pages(edge(k), edge(k + 1));
+    region.push_back(pl == kLockedByUs ? kLocked : pl == kPinnedByCaller ? kPinned : kFailed);
   };
   if (inplace) lock_region(0);
   HostLease res;

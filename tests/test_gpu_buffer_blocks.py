@@ -223,3 +223,44 @@ def test_in_place_and_staged_routes_agree(gpu, monkeypatch, env):
         offs, sizes = _cdc_like(rng, n)
         _check(data, offs, sizes)
     host.release_cache()
+
+
+def test_concurrent_in_place_calls_on_shared_pages(gpu):
+    """Threads indexing the same host buffer and overlapping slices of it at
+    once: each in-place call page-locks its regions; a region another call of
+    ours holds is bounced, never copied from while that call may unregister
+    it.  Every result equals the oracle's (sf_index_buffer and the list form)."""
+    import threading
+    n = 48 << 20
+    data = oracle.splitmix_bytes(n, 44)
+    rng = np.random.default_rng(44)
+    offs, sizes = _cdc_like(rng, n)
+    want_list = oracle.index_blocks(data, offs, sizes)
+    want_fixed = oracle.index_fixed(data, 4096)[2]
+    half = (n // 2) + 4096 * 3 + 100  # overlapping halves, sharing pages
+    sub = data[n // 2 - 12345:]
+    want_sub = oracle.index_fixed(sub, 4096)[2]
+    errors = []
+
+    def work(kind):
+        try:
+            for _ in range(3):
+                if kind == 0:
+                    rows, _ = host.index_buffer_blocks(data, offs, sizes)
+                    assert np.array_equal(rows["sha1"], want_list)
+                elif kind == 1:
+                    assert np.array_equal(host.index_buffer(data, 4096)["sha1"], want_fixed)
+                elif kind == 2:
+                    assert np.array_equal(host.index_buffer(sub, 4096)["sha1"], want_sub)
+                else:
+                    rows = host.index_buffer(data[:half], 4096)
+                    assert np.array_equal(rows["sha1"], oracle.index_fixed(data[:half], 4096)[2])
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errors.append((kind, e))
+
+    th = [threading.Thread(target=work, args=(k % 4,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
