@@ -6,8 +6,9 @@ stream (standing in for RCCL's receive kernel on rank 0) waits for that
 launch and then writes 7 x 40 MiB (what rank 0 receives per step at N = 8)
 with a device copy -- a CU-based blit, like RCCL's kernels; before the launch
 that reuses a table, the main stream waits for the side stream's work on it
-(what work.wait() does in bench.py).  Reported: ms per step for nbuf = 2, 3
-and no side work, interleaved."""
+(what work.wait() does in bench.py).  Reported: ms per step for nbuf = 2, 3,
+4, no side work, and nbuf = 3 with the receive on one step in 8 (the root
+rotating over 8 ranks, bench.py's default), interleaved."""
 import os
 import sys
 import time
@@ -20,7 +21,9 @@ from syncfast_amd import device  # noqa: E402
 GiB = 1 << 30
 
 
-def run(data, nbuf, steps, recv_bytes, side):
+def run(data, nbuf, steps, recv_bytes, side, every=1):
+    """every = k: this rank is the receiving root on one step in k (a root
+    that rotates over k ranks); every = 1: a fixed root."""
     bs = 4096
     nblk = data.numel() // bs
     digs = [torch.empty((nblk, 20), dtype=torch.uint8, device=data.device) for _ in range(nbuf)]
@@ -36,7 +39,7 @@ def run(data, nbuf, steps, recv_bytes, side):
         if done[b] is not None:
             main.wait_event(done[b])
         device.index_device(data, bs, out=digs[b], stream=main)
-        if side:
+        if side and i % every == 0:
             ev = torch.cuda.Event()
             ev.record(main)
             sstream.wait_event(ev)
@@ -58,9 +61,9 @@ def main():
     res = {}
     reps, steps = int(os.environ.get("SIM_REPS", "6")), int(os.environ.get("SIM_STEPS", "40"))
     for rep in range(reps):
-        for name, nbuf, side in (("no gather", 2, False), ("nbuf=2", 2, True), ("nbuf=3", 3, True),
-                                 ("nbuf=4", 4, True)):
-            ms = run(data, nbuf, steps, recv, side)
+        for name, nbuf, side, every in (("no gather", 2, False, 1), ("nbuf=2", 2, True, 1), ("nbuf=3", 3, True, 1),
+                                        ("nbuf=4", 4, True, 1), ("nbuf=3, root rotating over 8", 3, True, 8)):
+            ms = run(data, nbuf, steps, recv, side, every)
             res.setdefault(name, []).append(ms)
             print(f"rep {rep} {name}: {ms:.3f} ms/step", flush=True)
     for k, v in res.items():
