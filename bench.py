@@ -397,6 +397,11 @@ def main():
     if bstream is not None:
         bstream.finish()
     drain()
+    if gather and a.gather_root == "rotate":
+        # RCCL connects a pair of ranks on its first exchange: one gather to
+        # every root here (untimed), so no timed step pays for a connection
+        for r in range(world):
+            gather_digests(digs[0], total, bs, dst=r)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
