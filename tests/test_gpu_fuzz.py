@@ -178,3 +178,46 @@ def test_fuzz_block_set(gpu, case):
     with BlockSet(t, pres) as bset:
         got = bset.lookup(torch.from_numpy(q).to(gpu)).cpu().numpy()
     assert np.array_equal(got, oracle.block_lookup(table, present, q)), (n, pool.shape[0])
+
+
+@pytest.mark.parametrize("case", range(60))
+def test_fuzz_explicit_list_host_routes(gpu, case, tmp_path, monkeypatch):
+    """A host chunker's list over host memory or a file (sf_index_buffer_blocks
+    / sf_index_file_blocks): random block-size mixes (1-byte to 40 KiB blocks,
+    gaps, overlaps on odd cases, empty blocks), odd buffer starts, random stage
+    sizes, in place or staged, against the oracle's rows and blocks_hash."""
+    rng = np.random.default_rng(50_000 + case)
+    n = int(rng.choice([0, 1, 63, 64, 4097, int(rng.integers(1, 3 << 20))]))
+    raw = oracle.splitmix_bytes(n + 16, 60_000 + case)
+    shift = int(rng.integers(0, 16))
+    data = raw[shift:shift + n]
+    mean = float(rng.choice([1.5, 64, 3000, 8192, 20000]))
+    sizes, offs, pos = [], [], 0
+    while pos < n:
+        s = int(min(rng.geometric(1.0 / mean), 40_000, n - pos))
+        if case % 2 and rng.random() < 0.1:  # overlap or skip on odd cases
+            start = max(0, pos - int(rng.integers(0, 200)))
+            s = min(s, n - start)
+        else:
+            start = pos
+        if rng.random() < 0.03:
+            s = 0
+        offs.append(start)
+        sizes.append(s)
+        pos = max(pos, start + max(s, 1))
+    offs = np.asarray(offs, np.uint64)
+    sizes = np.asarray(sizes, np.uint32)
+    order = np.argsort(offs, kind="stable")  # non-decreasing offsets, as a chunker gives
+    offs, sizes = offs[order], sizes[order]
+    monkeypatch.setenv("SF_STREAM_STAGE_MIB", str(int(rng.choice([1, 2, 256]))))
+    if rng.random() < 0.3:
+        monkeypatch.setenv("SF_NO_HOSTREG", "1")
+    want = oracle.index_blocks(data, offs, sizes)
+    rows, bh = host.index_buffer_blocks(data, offs, sizes)
+    assert np.array_equal(rows["sha1"], want) and bh == oracle.blocks_hash(want), (n, mean)
+    assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+    if case % 3 == 0:
+        p = tmp_path / "f"
+        data.tofile(p)
+        rows2, bh2 = host.index_file_blocks(p, offs, sizes)
+        assert np.array_equal(rows2, rows) and bh2 == bh
