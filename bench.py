@@ -186,6 +186,15 @@ def cpu_baseline(nbytes_total, bs, budget_s):
                       f"oracle/sf_oracle.c SHA-1 (scalar C, no SHA-NI), 1 thread, SQLite excluded"}
 
 
+def cpu_model() -> str:
+    """The host CPU the baselines ran on (/proc/cpuinfo model name, x count)."""
+    try:
+        names = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")]
+    except OSError:
+        return "unknown"
+    return f"{names[0]} (x{len(names)} logical CPUs visible)" if names else "unknown"
+
+
 E2E_MAX = 8 * GiB  # host RAM bound of the end-to-end leg (config 4 at 256 GiB per GPU would not fit)
 
 
@@ -532,6 +541,7 @@ def main():
             "model": "613 VALU per 64-B SHA-1 compression (400 at 4 + 213 at 2 SIMD-cycles), 1024 SIMDs at 2.4 GHz; "
                      "the chip holds ~2.1 GHz under this load (DESIGN.md section 4)"},
         "cpu_baseline": cpu,
+        "cpu_model": cpu_model() if cpu is not None else None,  # state the CPU model
         "cpu_baseline_all_cores": cpu_all,
         "cpu_baseline_shani": cpu_ni,
         "cpu_baseline_shani_all_cores": cpu_ni_all,
