@@ -190,6 +190,16 @@ int sf_wire_file_blocks_device(const void *d_digests, uint64_t n_blocks, uint32_
                                uint64_t file_len, void *d_out, uint64_t cap, uint64_t *n_out,
                                void *stream);
 
+/* The FILE_BLOCK run of an explicit block list -- the reference's default,
+ * content-defined blocks, each with its own size -- built in HBM: message i =
+ * "FILE_BLOCK\n" + digest i + "\n" + decimal d_sizes[i] + "\n"
+ * (src/sync/ssh/proto.rs:162-166), back to back in list order.  The message
+ * offsets come from a scan on the device; the total is read back, so the call
+ * blocks until it is known.  *n_out = bytes (the need); SF_ENOSPC when cap is
+ * too small or d_out is NULL (a query). */
+int sf_wire_blocks_device(const void *d_digests, const uint32_t *d_sizes, uint64_t n_blocks,
+                          void *d_out, uint64_t cap, uint64_t *n_out, void *stream);
+
 /* The same FILE_BLOCK run written to a file descriptor (the SSH pipe of
  * src/sync/ssh/mod.rs, or a file), streamed: the device builds ~1M messages
  * at a time, each chunk comes back by DMA into pinned memory and is written

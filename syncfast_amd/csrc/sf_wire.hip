@@ -1,0 +1,113 @@
+// sf_wire.hip -- the FILE_BLOCK run of an explicit block list, built on the
+// device (its own translation unit: the SHA-1 kernels' code object in
+// sf_capi.hip stays as it is).
+//
+// The reference's source streams one FILE_BLOCK message per block after
+// FILE_START (src/sync/fs.rs:217-233, written by write_message,
+// src/sync/ssh/proto.rs:162-166): "FILE_BLOCK\n" + the 20 raw digest bytes +
+// "\n" + the block's size in decimal + "\n".  With the reference's default,
+// content-defined blocks every size differs, so message i starts at the sum
+// of the earlier messages' lengths (33 + digits(size)): one pass writes the
+// lengths, a rocprim inclusive scan turns them into end offsets, and one
+// thread per message writes it at its place.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <rocprim/device/device_scan.hpp>
+
+#include "sf_internal.hpp"
+
+namespace {
+
+__device__ __forceinline__ uint32_t digits10(uint32_t v) {
+  uint32_t d = 1;
+  while (v >= 10) { v /= 10; ++d; }
+  return d;
+}
+
+__global__ void __launch_bounds__(256) wire_len_kernel(const uint32_t* __restrict__ sizes, uint64_t n,
+                                                       uint64_t* __restrict__ lens) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) lens[i] = 33u + digits10(sizes[i]);  // 11 + 20 + 1 + digits + 1
+}
+
+__global__ void __launch_bounds__(256) wire_blocks_kernel(const uint8_t* __restrict__ digests,
+                                                          const uint32_t* __restrict__ sizes,
+                                                          const uint64_t* __restrict__ ends, uint64_t n,
+                                                          uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t v = sizes[i];
+  const uint32_t nd = digits10(v);
+  uint8_t* o = out + ends[i] - (33u + nd);
+  const char tag[11] = {'F', 'I', 'L', 'E', '_', 'B', 'L', 'O', 'C', 'K', '\n'};
+#pragma unroll
+  for (int k = 0; k < 11; ++k) o[k] = (uint8_t)tag[k];
+  const uint8_t* d = digests + i * 20;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) o[11 + k] = d[k];
+  o[31] = '\n';
+  for (int k = (int)nd - 1; k >= 0; --k) { o[32 + k] = (uint8_t)('0' + v % 10); v /= 10; }
+  o[32 + nd] = '\n';
+}
+
+constexpr uint64_t kWireMaxPerLaunch = 1ull << 30;  // messages per launch (grid x stays far below 2^31)
+
+}  // namespace
+
+extern "C" {
+
+int sf_wire_blocks_device(const void* d_digests, const uint32_t* d_sizes, uint64_t n_blocks, void* d_out,
+                          uint64_t cap, uint64_t* n_out, void* stream) {
+  using sfi::ceil_div;
+  if (n_out) *n_out = 0;
+  if (n_blocks == 0) return SF_OK;
+  if (!d_sizes) return SF_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // workspace on the stream: lengths, end offsets, scan temporary
+  size_t tmp = 0;
+  uint64_t* nul = nullptr;
+  if (rocprim::inclusive_scan(nullptr, tmp, nul, nul, (size_t)n_blocks, rocprim::plus<uint64_t>(), s) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return SF_ENODEV;
+  }
+  const size_t lb = (n_blocks * 8 + 255) & ~(size_t)255;
+  uint8_t* ws = nullptr;
+  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), 2 * lb + tmp + 8, s));
+  uint64_t* lens = reinterpret_cast<uint64_t*>(ws);
+  uint64_t* ends = reinterpret_cast<uint64_t*>(ws + lb);
+  int rc = SF_OK;
+  uint64_t total = 0;
+  do {
+    hipLaunchKernelGGL(wire_len_kernel, dim3((unsigned)ceil_div(n_blocks, 256)), dim3(256), 0, s, d_sizes, n_blocks,
+                       lens);
+    if ((rc = sfi::hip_err(hipGetLastError())) != SF_OK) break;
+    if (rocprim::inclusive_scan(ws + 2 * lb, tmp, lens, ends, (size_t)n_blocks, rocprim::plus<uint64_t>(), s) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      rc = SF_ENODEV;
+      break;
+    }
+    // the need is the last end offset: read back (this call blocks here)
+    if (hipMemcpyAsync(&total, ends + n_blocks - 1, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
+    }
+    if (n_out) *n_out = total;
+    if (total > cap || !d_out) { rc = SF_ENOSPC; break; }
+    if (!d_digests) { rc = SF_EINVAL; break; }
+    for (uint64_t first = 0; first < n_blocks && rc == SF_OK; first += kWireMaxPerLaunch) {
+      const uint64_t cnt = std::min(kWireMaxPerLaunch, n_blocks - first);
+      hipLaunchKernelGGL(wire_blocks_kernel, dim3((unsigned)ceil_div(cnt, 256)), dim3(256), 0, s,
+                         static_cast<const uint8_t*>(d_digests) + first * 20, d_sizes + first, ends + first, cnt,
+                         static_cast<uint8_t*>(d_out));
+      rc = sfi::hip_err(hipGetLastError());
+    }
+  } while (0);
+  (void)hipFreeAsync(ws, s);
+  return rc;
+}
+
+}  // extern "C"

@@ -170,6 +170,31 @@ def file_blocks_device(digests, block_size: int, file_len: int, stream=None):
     return out
 
 
+def blocks_device(digests, sizes, stream=None):
+    """FILE_BLOCK messages for an explicit block list (content-defined
+    blocks, each with its own size), built on the device from a uint8[n, 20]
+    HBM digest table and an int32/uint32[n] HBM size array (bit pattern taken
+    as uint32) -> uint8 HBM tensor (sf_wire_blocks_device)."""
+    from .device import _on, _require_device
+    import torch
+    _require_device(digests, "digests", torch.uint8)
+    n = digests.shape[0]
+    if sizes.numel() != n or sizes.dtype not in (torch.int32, torch.uint32) or sizes.device != digests.device:
+        raise ValueError("sizes must be one 32-bit size per digest, on the digests' device")
+    sizes = sizes.contiguous()
+    need = ctypes.c_uint64(0)
+    with _on(digests.device, stream):
+        s = torch.cuda.current_stream(digests.device).cuda_stream
+        rc = lib().sf_wire_blocks_device(None, sizes.data_ptr() if n else None, n, None, 0, ctypes.byref(need), s)
+        if rc not in (0, -28):
+            check(rc, "sf_wire_blocks_device")
+        out = torch.empty(need.value, dtype=torch.uint8, device=digests.device)
+        if need.value:
+            check(lib().sf_wire_blocks_device(digests.data_ptr(), sizes.data_ptr(), n, out.data_ptr(), out.numel(),
+                                              ctypes.byref(need), s), "sf_wire_blocks_device")
+    return out
+
+
 def file_blocks_to_fd(digests, block_size: int, file_len: int, fd: int, stream=None) -> int:
     """The FILE_BLOCK run of a fixed-tiled file written to a file descriptor
     (an SSH pipe or a file): built on the device in chunks, streamed back by

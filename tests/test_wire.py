@@ -1,4 +1,5 @@
 """Wire emission of signature tables (src/sync/ssh/proto.rs)."""
+import ctypes
 import numpy as np
 import pytest
 import torch
@@ -121,3 +122,68 @@ def test_device_run_parses_back_to_the_rows(gpu, n, bs):
     assert [m[0] for m in msgs] == ["FileBlock"] * len(want)
     assert [m[1].bytes for m in msgs] == [bytes(w) for w in want]
     assert [m[2] for m in msgs] == [int(x) for x in sizes]
+
+
+def test_blocks_device_validation_without_device():
+    from syncfast_amd import _lib
+    L = _lib.lib()
+    n = ctypes.c_uint64(7)
+    assert L.sf_wire_blocks_device(None, None, 0, None, 0, ctypes.byref(n), None) == 0 and n.value == 0
+    assert L.sf_wire_blocks_device(None, None, 3, None, 0, ctypes.byref(n), None) == _lib.SF_EINVAL
+
+
+@pytest.mark.gpu
+def test_blocks_device_reference_kat_blocks(gpu):
+    """The KAT file's three content-defined blocks (src/index.rs:765-792) as
+    the FILE_BLOCK run a source would send: sizes 11579, 32768, 546."""
+    digs = ["fb5ef7ebadd82c8085c5ff63823622bae0e263f6", "570d8b30fcfd585e4127b561f5ecd376ff4d0101",
+            "b9a8c2641af2cf8fd8f36a2456a3eaa95c029127"]
+    sizes = [11579, 32768, 546]
+    d = torch.tensor(np.frombuffer(bytes.fromhex("".join(digs)), np.uint8).reshape(3, 20).copy(), device=gpu)
+    got = wire.blocks_device(d, torch.tensor(sizes, dtype=torch.int32, device=gpu)).cpu().numpy().tobytes()
+    want = b"".join(wire.write_message("FileBlock", bytes.fromhex(h), s) for h, s in zip(digs, sizes))
+    assert got == want
+    assert [m[2] for m in wire.Parser().receive(got)] == sizes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 100_003])
+def test_blocks_device_matches_write_message(gpu, n):
+    rng = np.random.default_rng(n)
+    dig = rng.integers(0, 256, (n, 20), dtype=np.uint8)
+    # every digit count from 1 to 10 (u32 up to 4294967295), zero included
+    sizes = (rng.integers(0, 10, n) * 0 + 10 ** rng.integers(0, 10, n) * rng.integers(1, 10, n)).astype(np.uint64)
+    sizes = np.minimum(sizes, 4294967295).astype(np.uint32)
+    sizes[rng.random(n) < 0.05] = 0
+    if n > 1:
+        sizes[-1] = 4294967295
+    got = wire.blocks_device(torch.from_numpy(dig).to(gpu),
+                             torch.from_numpy(sizes.view(np.int32)).to(gpu)).cpu().numpy().tobytes()
+    want = b"".join(wire.write_message("FileBlock", bytes(d), int(s)) for d, s in zip(dig, sizes))
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_blocks_device_equals_fixed_form_and_parses_back(gpu):
+    n, bs = 4096 * 3000 + 77, 4096
+    data = oracle.splitmix_bytes(n, 5)
+    t = torch.from_numpy(data.copy()).to(gpu)
+    dig = device.index_device(t, bs)
+    nb = dig.shape[0]
+    sizes = torch.full((nb,), bs, dtype=torch.int32, device=gpu)
+    sizes[-1] = n - (nb - 1) * bs
+    run = wire.blocks_device(dig, sizes)
+    assert torch.equal(run, wire.file_blocks_device(dig, bs, n))
+    # a content-defined-like list: rows back through the parser
+    rng = np.random.default_rng(6)
+    cut = np.minimum(rng.geometric(1 / 8192, 4000), 32768).astype(np.uint64)
+    ends = np.cumsum(cut)
+    ends = ends[ends < n]
+    b = np.concatenate([[0], ends, [n]]).astype(np.uint64)
+    offs, szs = b[:-1], np.diff(b).astype(np.uint32)
+    d2 = device.index_device_blocks(t, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                                    torch.from_numpy(szs.astype(np.int32)).to(gpu))
+    run2 = wire.blocks_device(d2, torch.from_numpy(szs.view(np.int32)).to(gpu)).cpu().numpy().tobytes()
+    msgs = wire.Parser().receive(run2)
+    assert [m[2] for m in msgs] == szs.tolist()
+    assert [m[1].bytes for m in msgs] == [bytes(x) for x in oracle.index_blocks(data, offs, szs)]
