@@ -208,6 +208,13 @@ int sf_wire_blocks_device(const void *d_digests, const uint32_t *d_sizes, uint64
 int sf_wire_file_blocks_fd(const void *d_digests, uint64_t n_blocks, uint32_t block_size,
                            uint64_t file_len, int fd, uint64_t *n_written, void *stream);
 
+/* The explicit list's FILE_BLOCK run (sf_wire_blocks_device) streamed to a
+ * file descriptor in chunks of messages, each built on the device, copied
+ * back and written while the next is built.  *n_written = bytes written.
+ * Blocking. */
+int sf_wire_blocks_fd(const void *d_digests, const uint32_t *d_sizes, uint64_t n_blocks, int fd,
+                      uint64_t *n_written, void *stream);
+
 /* Deterministic synthetic input (bench / tests): bytes [start, start+len)
  * of the splitmix64 stream with this seed. */
 int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t start, void *stream);

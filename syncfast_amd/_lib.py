@@ -31,7 +31,7 @@ EXPORTED = (
     "sf_version", "sf_strerror", "sf_device_count", "sf_set_device", "sf_release_host_cache",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
-    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
+    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
@@ -84,6 +84,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]
     L.sf_wire_blocks_device.argtypes = [vp, vp, u64, vp, u64, pu64, vp]
+    L.sf_wire_blocks_fd.argtypes = [vp, vp, u64, i32, pu64, vp]
     L.sf_wire_file_blocks_fd.argtypes = [vp, u64, u32, u64, i32, pu64, vp]
     L.sf_index_buffer.argtypes = [vp, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
     L.sf_index_buffer_blocks.argtypes = [vp, u64, vp, vp, u64, ctypes.POINTER(BlockSig), vp]

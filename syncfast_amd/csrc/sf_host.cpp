@@ -361,6 +361,68 @@ static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks,
   return rc;
 }
 
+// The FILE_BLOCK run of an explicit list streamed to fd: chunks of
+// SF_WIRE_CHUNK messages, each built by sf_wire_blocks_device (lengths, scan,
+// scatter; it blocks until the chunk's size is known), copied back into a
+// pinned buffer and written while the next chunk is built.
+static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes, uint64_t n_blocks, int fd,
+                                  uint64_t* n_written, void* stream) {
+  if (n_written) *n_written = 0;
+  if (n_blocks == 0) return SF_OK;
+  if (!d_digests || !d_sizes || fd < 0) return SF_EINVAL;
+  const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
+  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : kWireChunk);
+  const uint64_t nchunks = ceil_div(n_blocks, per);
+  const uint64_t cap = std::min(per, n_blocks) * 43;  // 33 + at most 10 digits per message
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* ev;
+  void *dout[2], *pin[2];
+  hipEvent_t ready = nullptr;
+  uint64_t bytes_of[2] = {0, 0};
+  int rc = res.streams(st, ev);
+  for (int i = 0; i < 2 && rc == SF_OK; i++) {
+    rc = res.dev(i, cap, &dout[i]);
+    if (rc == SF_OK) rc = res.pin(i, cap, &pin[i]);
+  }
+  if (rc != SF_OK) return rc;
+  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  if (hipEventRecord(ready, as_stream(stream)) != hipSuccess ||  // digests and sizes are produced on the caller's stream
+      hipStreamWaitEvent(st[0], ready, 0) != hipSuccess || hipStreamWaitEvent(st[1], ready, 0) != hipSuccess)
+    rc = SF_ENODEV;
+  uint64_t written = 0;
+  auto flush = [&](int b) {
+    if (hipEventSynchronize(ev[b]) != hipSuccess) return SF_ENODEV;
+    const uint8_t* p = static_cast<const uint8_t*>(pin[b]);
+    for (uint64_t done = 0; done < bytes_of[b];) {
+      const ssize_t w = write(fd, p + done, bytes_of[b] - done);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return SF_EIO;
+      done += (uint64_t)w;
+      written += (uint64_t)w;
+    }
+    return SF_OK;
+  };
+  for (uint64_t k = 0; k < nchunks && rc == SF_OK; k++) {
+    const int b = (int)(k & 1);
+    if (k >= 2 && (rc = flush(b)) != SF_OK) break;
+    const uint64_t i0 = k * per, cnt = std::min(per, n_blocks - i0);
+    uint64_t bytes = 0;
+    if ((rc = sf_wire_blocks_device(static_cast<const uint8_t*>(d_digests) + i0 * 20, d_sizes + i0, cnt, dout[b], cap,
+                                    &bytes, st[b])) != SF_OK)
+      break;
+    bytes_of[b] = bytes;
+    if (hipMemcpyAsync(pin[b], dout[b], bytes, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+        hipEventRecord(ev[b], st[b]) != hipSuccess)
+      rc = SF_ENODEV;
+  }
+  for (uint64_t k = nchunks >= 2 ? nchunks - 2 : 0; k < nchunks && rc == SF_OK; k++) rc = flush((int)(k & 1));
+  for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(st[i]);
+  (void)hipEventDestroy(ready);
+  if (n_written) *n_written = written;
+  return rc;
+}
+
 }  // extern "C"
 
 namespace {
@@ -976,6 +1038,11 @@ extern "C" {
 
 int sf_release_host_cache(void) {
   return guarded([&] { return sf_release_host_cache_body(); });
+}
+
+int sf_wire_blocks_fd(const void* d_digests, const uint32_t* d_sizes, uint64_t n_blocks, int fd, uint64_t* n_written,
+                      void* stream) {
+  return guarded([&] { return sf_wire_blocks_fd_body(d_digests, d_sizes, n_blocks, fd, n_written, stream); });
 }
 
 int sf_wire_file_blocks_fd(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len, int fd,

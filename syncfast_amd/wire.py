@@ -195,6 +195,22 @@ def blocks_device(digests, sizes, stream=None):
     return out
 
 
+def blocks_to_fd(digests, sizes, fd: int, stream=None) -> int:
+    """The explicit list's FILE_BLOCK run written to a file descriptor, built
+    on the device in chunks and streamed back (sf_wire_blocks_fd).  Returns
+    the bytes written."""
+    import torch
+    n = digests.shape[0]
+    if sizes.numel() != n or sizes.dtype not in (torch.int32, torch.uint32) or sizes.device != digests.device:
+        raise ValueError("sizes must be one 32-bit size per digest, on the digests' device")
+    sizes = sizes.contiguous()
+    s = (stream or torch.cuda.current_stream(digests.device)).cuda_stream
+    out = ctypes.c_uint64(0)
+    check(lib().sf_wire_blocks_fd(digests.data_ptr() if n else None, sizes.data_ptr() if n else None, n, int(fd),
+                                  ctypes.byref(out), s), "sf_wire_blocks_fd")
+    return out.value
+
+
 def file_blocks_to_fd(digests, block_size: int, file_len: int, fd: int, stream=None) -> int:
     """The FILE_BLOCK run of a fixed-tiled file written to a file descriptor
     (an SSH pipe or a file): built on the device in chunks, streamed back by

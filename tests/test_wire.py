@@ -130,6 +130,8 @@ def test_blocks_device_validation_without_device():
     n = ctypes.c_uint64(7)
     assert L.sf_wire_blocks_device(None, None, 0, None, 0, ctypes.byref(n), None) == 0 and n.value == 0
     assert L.sf_wire_blocks_device(None, None, 3, None, 0, ctypes.byref(n), None) == _lib.SF_EINVAL
+    assert L.sf_wire_blocks_fd(None, None, 0, 1, ctypes.byref(n), None) == 0 and n.value == 0
+    assert L.sf_wire_blocks_fd(None, None, 3, 1, ctypes.byref(n), None) == _lib.SF_EINVAL
 
 
 @pytest.mark.gpu
@@ -187,3 +189,19 @@ def test_blocks_device_equals_fixed_form_and_parses_back(gpu):
     msgs = wire.Parser().receive(run2)
     assert [m[2] for m in msgs] == szs.tolist()
     assert [m[1].bytes for m in msgs] == [bytes(x) for x in oracle.index_blocks(data, offs, szs)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", ["1", "7", "1000", "0"])
+def test_blocks_to_fd_streams_the_device_run(gpu, tmp_path, monkeypatch, chunk):
+    if chunk != "0":
+        monkeypatch.setenv("SF_WIRE_CHUNK", chunk)
+    rng = np.random.default_rng(int(chunk) + 3)
+    n = 20_000 if chunk != "1" else 700
+    dig = torch.from_numpy(rng.integers(0, 256, (n, 20), dtype=np.uint8)).to(gpu)
+    sizes = torch.from_numpy(np.minimum(rng.geometric(1 / 8192, n), 32768).astype(np.int32)).to(gpu)
+    want = wire.blocks_device(dig, sizes).cpu().numpy().tobytes()
+    p = tmp_path / "run.bin"
+    with open(p, "wb") as f:
+        got = wire.blocks_to_fd(dig, sizes, f.fileno())
+    assert got == len(want) and p.read_bytes() == want
