@@ -17,6 +17,8 @@
  *     sf_index_file_blocks, which must agree);
  *     -s N: each file as N sf_index_file_range shards;
  *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
+ *     -v N: the same bytes cut by the host chunker (-C), hashed as a list in
+ *     HBM, the list's FILE_BLOCK run to stdout (sf_wire_blocks_fd);
  *     -L dst src: src's blocks looked up among dst's (sf_block_set_*)
  */
 #include <fcntl.h>
@@ -133,19 +135,13 @@ static int index_buffer_or_shards(const char *path, uint32_t bs, int shards) {
  * is Rust): a block ends after byte i when the little-endian word of bytes
  * i-3..i, times 2654435761 (mod 2^32), is below 2^19 (rate 2^-13, ~8 KiB
  * blocks), or when it reaches 32 KiB (src/index.rs:40-41). */
-static int index_cdc(const char *path) {
-    struct stat sb;
-    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;
-    const uint64_t len = (uint64_t)sb.st_size;
-    uint8_t *buf = malloc(len ? len : 1), bh[20];
+/* The stand-in chunker: (*offs, *sizes, *n) for buf[0, len), lists grown
+ * with realloc (caller frees). */
+static int cdc_cut(const uint8_t *buf, uint64_t len, uint64_t **offs_out, uint32_t **sizes_out, uint64_t *n_out) {
     uint64_t n = 0, cap = len / 4096 + 16;
     uint64_t *offs = malloc(cap * sizeof(uint64_t));
     uint32_t *sizes = malloc(cap * sizeof(uint32_t));
-    sf_block_sig *rows = NULL;
-    int rc = (buf && offs && sizes) ? SF_OK : SF_ENOMEM;
-    FILE *f = rc == SF_OK ? fopen(path, "rb") : NULL;
-    if (rc == SF_OK && (!f || fread(buf, 1, len, f) != len)) rc = SF_EIO;
-    if (f) fclose(f);
+    int rc = (offs && sizes) ? SF_OK : SF_ENOMEM;
     for (uint64_t start = 0, i = 0; rc == SF_OK && i < len; i++) {
         const uint32_t w = i >= 3 ? (uint32_t)buf[i - 3] | (uint32_t)buf[i - 2] << 8 | (uint32_t)buf[i - 1] << 16 |
                                         (uint32_t)buf[i] << 24
@@ -165,6 +161,25 @@ static int index_cdc(const char *path) {
             start = i + 1;
         }
     }
+    *offs_out = offs;
+    *sizes_out = sizes;
+    *n_out = n;
+    return rc;
+}
+
+static int index_cdc(const char *path) {
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;
+    const uint64_t len = (uint64_t)sb.st_size;
+    uint8_t *buf = malloc(len ? len : 1), bh[20];
+    uint64_t n = 0, *offs = NULL;
+    uint32_t *sizes = NULL;
+    sf_block_sig *rows = NULL;
+    int rc = buf ? SF_OK : SF_ENOMEM;
+    FILE *f = rc == SF_OK ? fopen(path, "rb") : NULL;
+    if (rc == SF_OK && (!f || fread(buf, 1, len, f) != len)) rc = SF_EIO;
+    if (f) fclose(f);
+    if (rc == SF_OK) rc = cdc_cut(buf, len, &offs, &sizes, &n);
     if (rc == SF_OK) rc = (rows = malloc((n ? n : 1) * sizeof(sf_block_sig))) ? SF_OK : SF_ENOMEM;
     if (rc == SF_OK) rc = sf_index_buffer_blocks(buf, len, offs, sizes, n, rows, bh);
     if (rc == SF_OK) {  /* the file form (pread windows) must give the same rows and blocks_hash */
@@ -180,6 +195,39 @@ static int index_cdc(const char *path) {
     free(offs);
     free(sizes);
     free(rows);
+    return rc;
+}
+
+/* -v N: the default mode's wire run from C: N synthetic bytes generated in
+ * HBM, cut on the host by the stand-in chunker, hashed on the device as an
+ * explicit list (sf_index_device_blocks), and the list's FILE_BLOCK run --
+ * every block with its own size -- streamed to stdout (sf_wire_blocks_fd). */
+static int wire_synthetic_cdc(uint64_t len) {
+    void *d_data = NULL, *d_dig = NULL, *d_offs = NULL, *d_sizes = NULL;
+    uint8_t *buf = malloc(len ? len : 1);
+    uint64_t n = 0, *offs = NULL, written = 0;
+    uint32_t *sizes = NULL;
+    int rc = (buf && hipMalloc(&d_data, len ? len : 1) == hipSuccess) ? SF_OK : SF_ENOMEM;
+    if (rc == SF_OK) rc = sf_fill_splitmix_device(d_data, len, 0x5EED0000ull, 0, NULL);
+    if (rc == SF_OK && len && hipMemcpy(buf, d_data, len, hipMemcpyDeviceToHost) != hipSuccess) rc = SF_ENODEV;
+    if (rc == SF_OK) rc = cdc_cut(buf, len, &offs, &sizes, &n);
+    if (rc == SF_OK && (hipMalloc(&d_dig, n ? n * 20 : 20) != hipSuccess ||
+                        hipMalloc(&d_offs, n ? n * 8 : 8) != hipSuccess || hipMalloc(&d_sizes, n ? n * 4 : 4) != hipSuccess))
+        rc = SF_ENOMEM;
+    if (rc == SF_OK && n &&
+        (hipMemcpy(d_offs, offs, n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(d_sizes, sizes, n * 4, hipMemcpyHostToDevice) != hipSuccess))
+        rc = SF_ENODEV;
+    if (rc == SF_OK) rc = sf_index_device_blocks(d_data, len, d_offs, d_sizes, n, d_dig, NULL, NULL);
+    if (rc == SF_OK) rc = sf_wire_blocks_fd(d_dig, d_sizes, n, 1, &written, NULL);
+    if (rc == SF_OK && n && written == 0) rc = SF_EIO;
+    if (d_data) (void)hipFree(d_data);
+    if (d_dig) (void)hipFree(d_dig);
+    if (d_offs) (void)hipFree(d_offs);
+    if (d_sizes) (void)hipFree(d_sizes);
+    free(buf);
+    free(offs);
+    free(sizes);
     return rc;
 }
 
@@ -285,20 +333,21 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0;
-    long long wire = -1;
+    long long wire = -1, wire_cdc = -1;
     int i = 1;
     for (; i < argc; i++) {
         if (i + 1 < argc && strcmp(argv[i], "-b") == 0) bs = (uint32_t)strtoul(argv[++i], NULL, 10);
         else if (i + 1 < argc && strcmp(argv[i], "-s") == 0) shards = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-w") == 0) wire = atoll(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-v") == 0) wire_cdc = atoll(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
         else if (strcmp(argv[i], "-L") == 0) lookup = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
         else if (strcmp(argv[i], "-C") == 0) cdc = 1;
         else break;
     }
-    if (i >= argc && wire < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -s shards] path... | -w bytes | -L dst src\n",
+    if (i >= argc && wire < 0 && wire_cdc < 0) {
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -s shards] path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
     }
@@ -307,6 +356,12 @@ int main(int argc, char **argv) {
     if (ndev == 0) {
         fprintf(stderr, "%s: no HIP device (syncfast_amd has no CPU path)\n", argv[0]);
         return 1;
+    }
+    if (wire_cdc >= 0) {
+        const int rc = wire_synthetic_cdc((uint64_t)wire_cdc);
+        if (rc != SF_OK) fprintf(stderr, "wire: %s\n", sf_strerror(rc));
+        sf_release_host_cache();
+        return rc != SF_OK;
     }
     if (wire >= 0) {
         const int rc = wire_synthetic((uint64_t)wire, bs);

@@ -163,3 +163,19 @@ def test_c_consumer_content_defined_blocks(gpu, tmp_path):
         assert got[name]["rows"] == rows and got[name]["bh"] == oracle.blocks_hash(dig).hex(), name
     assert [r[1] for r in got[str(tmp_path / "ones")]["rows"]] == [32768, 32768, 32768, 100_000 - 3 * 32768]
     assert len(got[str(tmp_path / "zeros")]["rows"]) == 50_000 - 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 5, 100_000, (3 << 20) + 17])
+def test_c_consumer_content_defined_wire_run(gpu, n):
+    # -v: bytes generated in HBM, cut by the host chunker, hashed as a list
+    # on the device and the list's FILE_BLOCK run streamed to stdout, from C
+    # -- equal to write_message over the oracle's digests and sizes
+    from syncfast_amd import wire
+    r = subprocess.run([_built(False), "-v", str(n)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    data = oracle.splitmix_bytes(n, 0x5EED0000)
+    offs, sizes = _cdc_cuts(data)
+    dig = oracle.index_blocks(data, np.asarray(offs, np.uint64), np.asarray(sizes, np.uint32))
+    want = b"".join(wire.write_message("FileBlock", bytes(d), int(s)) for d, s in zip(dig, sizes))
+    assert r.stdout == want
