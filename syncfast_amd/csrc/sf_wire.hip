@@ -80,9 +80,15 @@ int sf_wire_blocks_device(const void* d_digests, const uint32_t* d_sizes, uint64
   int rc = SF_OK;
   uint64_t total = 0;
   do {
-    hipLaunchKernelGGL(wire_len_kernel, dim3((unsigned)ceil_div(n_blocks, 256)), dim3(256), 0, s, d_sizes, n_blocks,
-                       lens);
-    if ((rc = sfi::hip_err(hipGetLastError())) != SF_OK) break;
+    // pieces of at most 2^30 messages per launch: a grid past 2^32
+    // work-items is not launched whole
+    for (uint64_t first = 0; first < n_blocks && rc == SF_OK; first += kWireMaxPerLaunch) {
+      const uint64_t cnt = std::min(kWireMaxPerLaunch, n_blocks - first);
+      hipLaunchKernelGGL(wire_len_kernel, dim3((unsigned)ceil_div(cnt, 256)), dim3(256), 0, s, d_sizes + first, cnt,
+                         lens + first);
+      rc = sfi::hip_err(hipGetLastError());
+    }
+    if (rc != SF_OK) break;
     if (rocprim::inclusive_scan(ws + 2 * lb, tmp, lens, ends, (size_t)n_blocks, rocprim::plus<uint64_t>(), s) !=
         hipSuccess) {
       (void)hipGetLastError();
