@@ -21,8 +21,9 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
                    time (HIP events on the launch stream) vs 8.0 TB/s HBM peak;
                    traffic = HBM bytes per launch from rocprofv3 PMC counters
                    (profiles/traffic.json, measured separately on the SAME
-                   kernels -- keyed by the SHA-256 of the library's gfx950
-                   code objects -- else null);
+                   kernel -- keyed by the SHA-256 of the headline kernel's
+                   machine code in the library's gfx950 code object -- else
+                   null);
   cpu_baseline  -- the C oracle (single-threaded SHA-1 port of the
                    reference loop) on a bounded sample of the same bytes, rank 0
                    at N=1 only; cpu_baseline_shani the same tiling with the
@@ -37,8 +38,13 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
 Launch: --gpus N > 1 without torchrun (no WORLD_SIZE in the environment)
 starts the N rank processes itself -- torch.distributed.run as a CHILD
 process, before anything here touches the GPU -- and exits with its status;
-rank 0 asserts that the process group holds N ranks.
+rank 0 asserts that the process group holds N ranks.  The process group has
+a timeout (--dist-timeout, 300 s): a gather that never completes ends the run
+with an error instead of hanging.  At N > 1 the line carries a `multi` block:
+every rank's kernel time, how long each rank's stream waited for the gathers
+(as receiving rank and as sender), and the world size the backend reports.
 """
+import datetime
 import argparse
 import hashlib
 import json
@@ -106,6 +112,8 @@ def parse():
                    help="also compute the opt-in fused Adler-32 weak sum per block (not in the reference; "
                         "configs 2 and 5 only); not the headline")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds before a stuck collective fails the run (init_process_group timeout)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--check-launch", action="store_true",
                    help="launcher check only (no GPU): every rank joins the process group (gloo), rank 0 "
@@ -127,16 +135,45 @@ def self_launch(a) -> int:
     return subprocess.call(cmd)
 
 
+def multi_block(dist, torch, dev, a, rank, world, kern_ms, waits, roots, backend):
+    """The `multi` block of an N > 1 line: every rank's kernel time and how
+    long its stream stood waiting for gathers, split by whether the rank was
+    the gather's receiving rank (waits[j] is the wait before step j's table
+    could be reused, roots[j] that gather's destination).  One all_gather of
+    4 numbers per rank."""
+    recv = [w for w, r in zip(waits, roots) if r == rank]
+    send = [w for w, r in zip(waits, roots) if r != rank]
+    mine = torch.tensor([kern_ms, sum(recv) / max(1, len(recv)), sum(send) / max(1, len(send)),
+                         float(len(recv))], dtype=torch.float64, device=dev)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [v.cpu().tolist() for v in allv]
+    k = [r[0] for r in rows]
+    return {"world": dist.get_world_size(), "backend": backend,
+            "kernel_ms": {"max": round(max(k), 4), "min": round(min(k), 4), "per_rank": [round(x, 4) for x in k]},
+            "gather_wait_ms_as_root": [round(r[1], 4) for r in rows],
+            "gather_wait_ms_as_sender": [round(r[2], 4) for r in rows],
+            "steps_as_root": [int(r[3]) for r in rows],
+            "note": "wait = time the rank's stream stood still before reusing a table its gather was still "
+                    "reading (HIP events around work.wait()), per gather, averaged"}
+
+
 def check_launch(a, world, rank) -> None:
+    """CPU-only rehearsal of the N-rank launch (gloo): every rank joins, the
+    world size is checked, and rank 0 prints the `multi` block built from
+    stand-in per-rank numbers (the kernel is not run without a GPU)."""
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=a.dist_timeout))
     seen = torch.ones(1)
     dist.all_reduce(seen)
     assert dist.get_world_size() == world == a.gpus and int(seen.item()) == a.gpus, (world, a.gpus, seen)
+    roots = [i % world for i in range(a.steps)]
+    multi = multi_block(dist, torch, torch.device("cpu"), a, rank, world, float(rank + 1), [0.0] * a.steps, roots,
+                        "gloo")
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item())}),
-              flush=True)
+        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item()),
+                          "multi": multi}), flush=True)
     dist.destroy_process_group()
 
 
@@ -300,10 +337,11 @@ def main():
     torch.cuda.set_device(dev)
     distributed = world > 1
     if distributed:
+        tmo = datetime.timedelta(seconds=a.dist_timeout)  # a stuck gather fails the run, never hangs it
         if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(a.dist_backend)
+            dist.init_process_group(a.dist_backend, timeout=tmo)
         # every rank joined and the communicator carries data: N ranks, N ones
         ones = torch.ones(1, device=dev) if a.dist_backend == "nccl" else torch.ones(1)
         dist.all_reduce(ones)
@@ -345,6 +383,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
     bstream = device.BatchStream(len(files), flen, bs, stream=stream) if files and a.c3_mode == "stream" else None
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # gather waits: events on the launch stream around work.wait() of every
+    # timed step's gather (multi block), with that gather's receiving rank
+    wait_ev, wait_root = [], []
     pending = [None] * nbuf
     last_table = [None]
     last_hashes = [None]  # batch stream: blocks_hash of the latest finished batch
@@ -360,13 +401,24 @@ def main():
             return 0
         return ((i - (a.steps - 1)) if timed else i) % world
 
+    def wait_gather(b, timed):
+        work, finish, j, r = pending[b]
+        if timed and j >= 0:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            work.wait()
+            e1.record(stream)
+            wait_ev.append((e0, e1))
+            wait_root.append(r)
+        else:
+            work.wait()
+        last_table[0] = finish  # concatenated only once, after the timed loop
+        pending[b] = None
+
     def step(i, timed):
         b = i % nbuf
         if pending[b] is not None:  # the gather that reads digs[b] must be done
-            work, finish, _ = pending[b]
-            work.wait()
-            last_table[0] = finish  # concatenated only once, after the timed loop
-            pending[b] = None
+            wait_gather(b, timed)
         if timed:
             ev[i][0].record(stream)
         if weaks is not None:
@@ -383,15 +435,13 @@ def main():
         if timed:
             ev[i][1].record(stream)
         if gather:
-            pending[b] = gather_digests(digs[b], total, bs, dst=root(i, timed), async_op=True) + (i,)
+            r = root(i, timed)
+            pending[b] = gather_digests(digs[b], total, bs, dst=r, async_op=True) + ((i if timed else -1), r)
 
-    def drain():
+    def drain(timed=False):
         # in step order, so last_table ends as the last step's gather (rank 0's)
         for b in sorted((b for b in range(nbuf) if pending[b] is not None), key=lambda b: pending[b][2]):
-            work, finish, _ = pending[b]
-            work.wait()
-            last_table[0] = finish
-            pending[b] = None
+            wait_gather(b, timed)
 
     # Setup (not a step): clock ramp, untimed, no gather.
     t_ramp = time.perf_counter()
@@ -422,7 +472,7 @@ def main():
         fin = bstream.finish()
         if fin:
             last_hashes[0] = fin[-1]
-    drain()
+    drain(True)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -436,6 +486,11 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
     t = float(elapsed.item())
+    multi = None
+    if distributed:
+        waits = [e0.elapsed_time(e1) for e0, e1 in wait_ev]
+        multi = multi_block(dist, torch, dev if a.dist_backend == "nccl" else torch.device("cpu"), a, rank, world,
+                            kern_ms, waits, wait_root, "rccl" if a.dist_backend == "nccl" else a.dist_backend)
     kern_ms = float(kt.item())
     dig = digs[(a.steps - 1) % nbuf]
     gathered = last_table[0]() if last_table[0] is not None else None
@@ -480,18 +535,19 @@ def main():
     if weaks is not None:  # + 4 B weak sum written per block
         alg_bytes += nblk * 4
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    # PMC traffic of the same kernels (same gfx950 code objects; else null:
-    # numbers from other kernels are stale).
-    from syncfast_amd._lib import code_object_sha256
+    # PMC traffic of the same kernel (same machine code of the headline
+    # kernel; else null: numbers from other code are stale).
+    from syncfast_amd._lib import code_object_sha256, kernel_code_sha256
     traffic = None
     build = lib_sha256()
     kernels = code_object_sha256()
+    kcode = kernel_code_sha256()
     try:
         with open(a.traffic_file) as f:
             tr = json.load(f)
         key = f"config{a.config}"
         ent = tr.get(key, {})
-        if ent.get("shard_bytes") == shard and ent.get("code_object_sha256") == kernels and not a.weak:
+        if ent.get("shard_bytes") == shard and ent.get("kernel_code_sha256") == kcode and not a.weak:
             traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
@@ -548,6 +604,8 @@ def main():
         "config1": config1_probe() if world == 1 else None,
         "lib_sha256": build,
         "code_object_sha256": kernels,
+        "kernel_code_sha256": kcode,
+        "multi": multi,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
         "e2e_host_buffer": e2e,

@@ -1,0 +1,38 @@
+/* syncfast_amd_test.h -- test hooks of libsyncfast_amd (not part of the
+ * drop-in surface; no reference interface corresponds).
+ *
+ * The library reads its environment knobs once, when it is loaded
+ * (syncfast_amd/csrc/sf_knobs.cpp); nothing on a launch or copy path reads
+ * the environment.  A test that needs another value inside the same process
+ * sets it here.  Names are the environment variables' (INTEGRATION.md,
+ * "Environment knobs"): SF_* performance knobs and SF_TEST_* hooks.
+ */
+#ifndef SYNCFAST_AMD_TEST_H
+#define SYNCFAST_AMD_TEST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Set knob `name` to `value`; the previous value goes to *old_value (may be
+ * NULL).  SF_EINVAL for an unknown name.  Not synchronised with calls in
+ * flight on other threads: set knobs between calls. */
+int sf_test_set_knob(const char* name, int64_t value, int64_t* old_value);
+
+/* Current value of knob `name`. */
+int sf_test_get_knob(const char* name, int64_t* value);
+
+/* Process-wide counters of the routes the host entry points took:
+ *   "pages_locked"      caller ranges the library page-locked (hipHostRegister)
+ *   "not_anon_refused"  caller ranges it did not page-lock because they are not
+ *                       private anonymous memory (a file mapping, shared
+ *                       memory): those are copied through the pinned stages. */
+int sf_test_get_stat(const char* name, int64_t* value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SYNCFAST_AMD_TEST_H */

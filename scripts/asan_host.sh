@@ -21,7 +21,7 @@ for i in range(300):
 EOF
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:exitcode=99
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1:exitcode=98
-export SF_STREAM_STAGE_MIB=1
+export SF_TEST_STREAM_STAGE_MIB=1
 rc=0
 run() {  # name cmd...  (both builds, same input, outputs compared)
   local name=$1; shift
@@ -39,8 +39,8 @@ run stdin -b 4096 - || rc=1
 run buffer -B -b 4096 "$W"/f0* || rc=1
 run buffer_small -B -b 64 "$W"/f0[0-7] || rc=1
 run shards -s 3 -b 4096 "$W"/f0* || rc=1
-SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 run inplace -b 4096 "$W"/f0* || rc=1
-SF_FILE_INPLACE=1 SF_INPLACE_MIN_MIB=1 SF_INPLACE_FAIL_AT=1 run inplace_bounce -b 4096 "$W"/f0* || rc=1
+SF_INPLACE_MIN_MIB=1 run inplace -B -b 4096 "$W"/f0* || rc=1
+SF_INPLACE_MIN_MIB=1 SF_TEST_INPLACE_FAIL_AT=1 run inplace_bounce -B -b 4096 "$W"/f0* || rc=1
 run wire -w 104857601 -b 4096 || rc=1
 run wire_bs1000 -w 3000001 -b 1000 || rc=1
 run lookup -L -b 4096 "$W"/f09 "$W"/f09 || rc=1

@@ -9,6 +9,7 @@ import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 import numpy as np  # noqa: E402
 
 from syncfast_amd import host  # noqa: E402
@@ -48,7 +49,7 @@ def main():
         # next stage) vs 0 (plain pread)
         for rep in range(2):
           for adv in ("1", "0"):
-            os.environ["SF_FADVISE"] = adv
+            set_knob("SF_FADVISE", int(adv))
             fd = os.open(path, os.O_RDONLY)
             os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
             os.close(fd)

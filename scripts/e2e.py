@@ -54,17 +54,13 @@ def main():
         f.write(data.tobytes())
         path = f.name
     try:
-        # default = pread pipeline (stages read by 8 threads, rows + blocks_hash
-        # per stage); SF_FILE_INPLACE=1 = the opt-in mapped + page-locked route
-        inpl = {"SF_FILE_INPLACE": "1"}
-        for i, env in enumerate([{}, {}, inpl, {}, inpl, {}, inpl]):
-            os.environ.update(env)
+        # the pread pipeline (stages read by 16 threads, rows + blocks_hash per
+        # stage); the file is never mapped and page-locked
+        for i in range(4):
             t0 = time.perf_counter()
             rows, bh = host.index_file(path, 4096)
             t = time.perf_counter() - t0
-            for k in env:
-                del os.environ[k]
-            what = "cold-ish" if i == 0 else "page cache, " + ("in place (opt-in)" if env else "pread pipeline")
+            what = "cold-ish" if i == 0 else "page cache, pread pipeline"
             print(f"sf_index_file {n / GiB:.0f} GiB ({what}), incl. blocks_hash:", rate(n, t), flush=True)
     finally:
         os.unlink(path)
@@ -76,6 +72,7 @@ def wire_rate():
     """FILE_BLOCK run of config 2's table (2^21 blocks) streamed to a file
     descriptor (/dev/null: device build + D2H + write syscalls)."""
     from syncfast_amd import device, wire
+    from syncfast_amd._lib import set_knob
     n = 8 << 30
     t = device.splitmix_tensor(n, 0x5EED0000)
     dig = device.index_device(t, 4096)
@@ -83,14 +80,14 @@ def wire_rate():
     with open("/dev/null", "wb") as f:
         wire.file_blocks_to_fd(dig, 4096, n, f.fileno())  # warm up
         for rep in range(2):
-            for chunk in ("65536", "262144", "1048576"):  # messages per chunk (SF_WIRE_CHUNK; default 262144)
-                os.environ["SF_WIRE_CHUNK"] = chunk
+            for chunk in ("65536", "262144", "1048576"):  # messages per chunk (SF_TEST_WIRE_CHUNK; default 262144)
+                set_knob("SF_TEST_WIRE_CHUNK", int(chunk))
                 t0 = time.perf_counter()
                 nbytes = wire.file_blocks_to_fd(dig, 4096, n, f.fileno())
                 dt = time.perf_counter() - t0
                 print(f"wire: FILE_BLOCK run of 2^21 blocks ({nbytes / 1e6:.1f} MB) to an fd, chunk {chunk}: "
                       f"{nbytes / dt / 1e9:.2f} GB/s ({dig.shape[0] / dt / 1e6:.1f} M messages/s)", flush=True)
-        del os.environ["SF_WIRE_CHUNK"]
+        set_knob("SF_TEST_WIRE_CHUNK", 0)
 
 
 def many_files(data, d):

@@ -12,6 +12,7 @@ import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 import numpy as np  # noqa: E402
 
 from syncfast_amd import host  # noqa: E402
@@ -40,7 +41,7 @@ def main():
         small.append(k)
         left -= k
     cases = [("0-200 KiB files", small), ("8 MiB files", [8 << 20] * (n // (8 << 20)))]
-    os.environ["SF_TRACE"] = "1"
+    set_knob("SF_TRACE", 1)
     for name, sizes in cases:
         root = tempfile.mkdtemp(dir=os.environ.get("E2E_DIR", "/tmp"))
         try:

@@ -6,6 +6,7 @@ import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 import numpy as np  # noqa: E402
 
 from syncfast_amd import host  # noqa: E402
@@ -26,7 +27,7 @@ try:
                 f.write(b[k * MiB:k * MiB + mib * MiB].tobytes() if k + mib <= 64 else b[:mib * MiB].tobytes())
             paths.append(p)
         for knob in ("1024", "0", "1024", "0"):
-            os.environ["SF_INPLACE_MIN_MIB"] = knob
+            set_knob("SF_INPLACE_MIN_MIB", int(knob))
             name = "staged " if knob != "0" else "in place"
             t0 = time.perf_counter()
             for k in range(16):

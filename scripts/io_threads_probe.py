@@ -6,6 +6,7 @@ import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 import numpy as np  # noqa: E402
 
 from syncfast_amd import host  # noqa: E402
@@ -31,7 +32,7 @@ with tempfile.TemporaryDirectory(dir=os.environ.get("E2E_DIR", "/tmp")) as td:
     for name, paths, nbytes in (("0-200 KiB", small, off), ("8 MiB", big, 1 << 30)):
         host.index_files(paths, 4096)
         for th in ("8", "12", "16", "24", "8", "12", "16", "24"):
-            os.environ["SF_IO_THREADS"] = th
+            set_knob("SF_IO_THREADS", int(th))
             t0 = time.perf_counter()
             host.index_files(paths, 4096)
             t = time.perf_counter() - t0

@@ -5,8 +5,9 @@ are in KiB; on gfx950 FETCH_SIZE reports exactly half the bytes of a wide
 coalesced streaming read (16 B/lane loads and buffer_load ... lds alike), so it
 is doubled; WRITE_SIZE is exact for streaming stores.  Averages over every
 launch of the SHA-1 kernel in the pass.  The entry records the SHA-256 of the
-library the passes ran and of its gfx950 code objects (bench.py reports traffic
-only for the same code objects).  Only the full-shard launches count (the
+library the passes ran, of its gfx950 code objects and of the headline
+kernel's machine code (bench.py reports traffic only for the same kernel
+code).  Only the full-shard launches count (the
 largest grid of the pass).
 
 usage: python scripts/pmc_traffic.py FETCH_CSV WRITE_CSV CONFIG_KEY SHARD_BYTES [OUT]
@@ -18,7 +19,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-from syncfast_amd._lib import code_object_sha256  # noqa: E402
+from syncfast_amd._lib import code_object_sha256, kernel_code_sha256  # noqa: E402
 
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "syncfast_amd", "lib", "libsyncfast_amd.so")
 
@@ -48,6 +49,7 @@ def main():
                  "raw_kib": {"FETCH_SIZE": f, "WRITE_SIZE": w},
                  "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
                  "code_object_sha256": code_object_sha256(LIB),
+                 "kernel_code_sha256": kernel_code_sha256(LIB),
                  "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"}
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data[key]))

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 from syncfast_amd.device import fill_splitmix, index_device, index_device_blocks  # noqa: E402
 
 GiB = 1 << 30
@@ -105,9 +106,9 @@ def main():
             modes = [("1", b) for b in ("2", "3", "4", "5", "6")]
         for (name, (o, z)), (srt, cb) in [(c, m) for c in cases.items() for m in modes]:
             # SF_TABLE_SORT: 0 = list order, 1 = blocks sorted by length (the default from 2^17 blocks)
-            os.environ["SF_TABLE_SORT"] = srt
+            set_knob("SF_TEST_TABLE_SORT", int(srt))
             if cb:
-                os.environ["SF_TABLE_CLASS_BITS"] = cb
+                set_knob("SF_TABLE_CLASS_BITS", int(cb))
             name = name + ("_sorted" if srt == "1" else "") + (f"_m{cb}" if cb else "")
             to = torch.from_numpy(o).to(dev)
             tz = torch.from_numpy(z.astype(np.int32)).to(dev)

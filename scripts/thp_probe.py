@@ -17,6 +17,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from syncfast_amd._lib import set_knob  # noqa: E402  (knobs are latched at load)
 
 
 def child(d):
@@ -36,9 +37,9 @@ def child(d):
             ("sf_index_files small", lambda: host.index_files(small, 4096), sum(map(os.path.getsize, small))),
             ("sf_index_buffer staged 4 GiB", lambda: host.index_buffer(buf, 4096), n_big)):
         if name.startswith("sf_index_buffer"):
-            os.environ["SF_NO_HOSTREG"] = "1"
+            set_knob("SF_NO_HOSTREG", 1)
         best = min(_t(fn) for _ in range(3))
-        os.environ.pop("SF_NO_HOSTREG", None)
+        set_knob("SF_NO_HOSTREG", 0)
         out[name] = nbytes / best / 1e9
     print(" | ".join(f"{k}: {v:.2f} GB/s" for k, v in out.items()), flush=True)
 

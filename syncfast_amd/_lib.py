@@ -35,6 +35,8 @@ EXPORTED = (
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
+# Test hooks (include/syncfast_amd_test.h): knobs latched at load, route counters.
+EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat")
 
 
 class SfError(OSError):
@@ -101,7 +103,11 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_block_set_build.argtypes = [vp, vp, u64, ctypes.POINTER(vp), vp]
     L.sf_block_set_lookup.argtypes = [vp, vp, u64, vp, vp]
     L.sf_block_set_free.argtypes = [vp, vp]
-    for name in EXPORTED:
+    pi64 = ctypes.POINTER(ctypes.c_int64)
+    L.sf_test_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int64, pi64]
+    L.sf_test_get_knob.argtypes = [ctypes.c_char_p, pi64]
+    L.sf_test_get_stat.argtypes = [ctypes.c_char_p, pi64]
+    for name in EXPORTED + EXPORTED_TEST:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int
     L.sf_free_rows.restype = None
@@ -131,6 +137,94 @@ def _strerror(code: int) -> str:
 def check(rc: int, what: str = "") -> None:
     if rc != SF_OK:
         raise SfError(rc, what)
+
+
+def get_knob(name: str) -> int:
+    """Current value of a library knob (latched from the environment when the
+    library was loaded; include/syncfast_amd_test.h)."""
+    v = ctypes.c_int64()
+    check(lib().sf_test_get_knob(name.encode(), ctypes.byref(v)), name)
+    return v.value
+
+
+def set_knob(name: str, value: int) -> int:
+    """Set a library knob (test hook); returns the previous value."""
+    old = ctypes.c_int64()
+    check(lib().sf_test_set_knob(name.encode(), int(value), ctypes.byref(old)), name)
+    return old.value
+
+
+def get_stat(name: str) -> int:
+    """A route counter of the host entry points ("pages_locked",
+    "not_anon_refused")."""
+    v = ctypes.c_int64()
+    check(lib().sf_test_get_stat(name.encode(), ctypes.byref(v)), name)
+    return v.value
+
+
+def _code_objects(path: str):
+    """(triple, bytes) of every gfx950 code object in the library's
+    .hip_fatbin section (one clang offload bundle per GPU translation unit)."""
+    import struct
+    with open(path or LIB_PATH, "rb") as f:
+        b = f.read()
+    if b[:4] != b"\x7fELF" or b[4] != 2:
+        raise ValueError("not an ELF64 library")
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stro = secs[shstrndx][4]
+    fat = None
+    for sec in secs:
+        name = b[stro + sec[0]: b.index(b"\0", stro + sec[0])]
+        if name == b".hip_fatbin":
+            fat = b[sec[4]: sec[4] + sec[5]]
+    if fat is None:
+        raise ValueError("no .hip_fatbin section")
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos = fat.find(magic)
+    while pos >= 0:  # bundle: magic, u64 entries, then (u64 offset, u64 size, u64 triple length, triple)
+        n, = struct.unpack_from("<Q", fat, pos + len(magic))
+        p = pos + len(magic) + 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fat, p)
+            triple = fat[p + 24: p + 24 + tlen]
+            p += 24 + tlen
+            if triple.startswith(b"hipv4-amdgcn"):
+                yield triple, fat[pos + off: pos + off + size]
+        pos = fat.find(magic, pos + 1)
+
+
+def kernel_code_sha256(path: str = None,
+                       symbol: str = "_ZN2sf17sha1_fixed_kernelILi128ELi1ELb0EEEvPKhmjmPhNS_11PadScheduleEPj") -> str:
+    """SHA-256 of one kernel's machine code (its bytes in the gfx950 code
+    object's .text, located through .symtab): what the GPU runs for that
+    kernel.  Other kernels of the same translation unit can change without
+    changing it.  bench.py keys the PMC traffic of profiles/traffic.json on it
+    for the headline kernel (sha1_fixed_kernel<128, 1, false>)."""
+    import hashlib
+    import struct
+    for _, co in _code_objects(path):
+        if co[:4] != b"\x7fELF":
+            continue
+        shoff, = struct.unpack_from("<Q", co, 0x28)
+        shentsize, shnum, shstrndx = struct.unpack_from("<HHH", co, 0x3A)
+        secs = [struct.unpack_from("<IIQQQQIIQQ", co, shoff + i * shentsize) for i in range(shnum)]
+        stro = secs[shstrndx][4]
+        names = [co[stro + s[0]: co.index(b"\0", stro + s[0])] for s in secs]
+        if b".symtab" not in names:
+            continue
+        symtab = secs[names.index(b".symtab")]
+        strtab = secs[symtab[6]]  # sh_link
+        for i in range(symtab[5] // 24):
+            st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
+                "<IBBHQQ", co, symtab[4] + 24 * i)
+            nm = co[strtab[4] + st_name: co.index(b"\0", strtab[4] + st_name)]
+            if nm == symbol.encode() and st_size:
+                sec = secs[st_shndx]  # (name, type, flags, addr, offset, size, ...)
+                start = sec[4] + (st_value - sec[3])
+                return hashlib.sha256(co[start: start + st_size]).hexdigest()
+    raise ValueError(f"no code object defines {symbol}")
 
 
 def code_object_sha256(path: str = None, kernel: bytes = b"sha1_fixed_kernel") -> str:

@@ -40,12 +40,11 @@ inline int variant_choice() {
 // larger tables -- reachable only with tiny blocks, e.g. 16-B blocks over
 // 64 GiB -- are hashed as several launches over consecutive block ranges
 // (blocks are independent).  A multiple of 16, so every piece of a 16-B
-// aligned fixed tiling stays 16-B aligned.  SF_LAUNCH_MAX_BLOCKS lowers it
-// (test knob: exercises the split at small sizes).
+// aligned fixed tiling stays 16-B aligned.  SF_TEST_LAUNCH_MAX_BLOCKS lowers
+// it (test hook: exercises the split at small sizes).
 inline uint64_t launch_max_blocks() {
-  const char* e = getenv("SF_LAUNCH_MAX_BLOCKS");
-  const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-  return v ? std::max<uint64_t>(16, v & ~15ull) : (1ull << 31);
+  const int64_t v = knob(K_TEST_LAUNCH_MAX_BLOCKS);
+  return v > 0 ? std::max<uint64_t>(16, (uint64_t)v & ~15ull) : (1ull << 31);
 }
 
 inline unsigned grid_for_blocks(uint64_t nblocks) {
@@ -131,10 +130,10 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
 // list order against 1834 GiB/s sorted (scripts/ragged_probe.py).  Below a
 // few waves per wave slot the sort cannot shorten the launch (every wave is
 // resident at once and the longest block sets the time), so small lists keep
-// their order.  SF_TABLE_SORT=0 / 1 never / always sorts (test knob).
+// their order.  SF_TEST_TABLE_SORT=0 / 1 never / always sorts (test hook).
 inline uint64_t table_sort_min() {
-  const char* e = getenv("SF_TABLE_SORT");
-  if (e) return atoi(e) ? 1 : ~0ull;
+  const int64_t v = knob(K_TEST_TABLE_SORT);
+  if (v >= 0) return v ? 1 : ~0ull;
   return 1ull << 17;
 }
 constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
@@ -145,8 +144,8 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.
 // nullptr (unsorted launch) if anything fails.
 uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
   *ws_out = nullptr;
-  const char* me = getenv("SF_TABLE_CLASS_BITS");  // mantissa bits of the length class, 1..6 (A/B knob)
-  const uint32_t mbits = me ? (uint32_t)std::min(6, std::max(1, atoi(me))) : 6u;
+  // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
+  const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
   const unsigned kbits = 5u + mbits;  // class < 32 << mbits
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   uint16_t *kin = nullptr, *kout = nullptr;
@@ -222,8 +221,8 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
 // workgroups per CU); larger batches (> 256 x 256 files) take the unstaged
 // path, which never waits.  (b): d_status (device int32) receives
 // SF_ETIMEDOUT; with d_status == NULL the unstaged path is taken.
-// SF_CHAIN_SPIN_LIMIT (test knob) bounds the polls of each wait (default
-// 2^24, several seconds).
+// SF_TEST_CHAIN_SPIN_LIMIT (test hook) bounds the polls of each wait
+// (default 2^24, several seconds).
 inline unsigned device_cus() {
   static std::atomic<int> cached{0};
   int v = cached.load();
@@ -239,15 +238,15 @@ inline unsigned device_cus() {
 }
 
 inline uint32_t chain_spin_limit() {
-  const char* e = getenv("SF_CHAIN_SPIN_LIMIT");
-  return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 24);
+  const int64_t v = knob(K_TEST_CHAIN_SPIN_LIMIT);
+  return v >= 0 ? (uint32_t)std::min<int64_t>(v, 0xFFFFFFFFll) : (1u << 24);
 }
 
 int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
                  uint8_t* fh, int* d_status, hipStream_t s) {
   int S = 1;
-  const char* se = getenv("SF_STAGES");  // A/B knob; default up to 16 stages
-  const int smax = se ? std::max(1, atoi(se)) : 16;
+  const int64_t sk = knob(K_TEST_STAGES);  // SF_TEST_STAGES (test hook); default up to 16 stages
+  const int smax = sk > 0 ? (int)std::min<int64_t>(sk, 32) : 16;
   for (int cand : {32, 16, 8, 4, 2})
     if (cand <= smax && nbf % (64ull * cand) == 0 && ((uint64_t)nfiles * (nbf / cand)) % 64 == 0) {
       S = cand;

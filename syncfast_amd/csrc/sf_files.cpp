@@ -6,7 +6,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -31,8 +30,7 @@ struct Trace {
   std::chrono::steady_clock::time_point t0, last;
   double stat_ms = 0, big_ms = 0, wait_ms = 0, harvest_ms = 0, read_ms = 0, issue_ms = 0;
   Trace() {
-    const char* e = getenv("SF_TRACE");
-    on = e && atoi(e);
+    on = knob(K_TRACE) != 0;
     t0 = last = std::chrono::steady_clock::now();
   }
   void lap(double& acc) {
@@ -58,79 +56,16 @@ struct FileStage {
   uint64_t rows = 0;
 };
 
-// Page-cache-resident large files of a stage, mapped and page-locked in place
-// so their bytes go to the device by DMA straight from the page cache (no
-// pread copy into the pinned stage).  Released once the stage's copies are
-// done (its event has completed, or the streams are synchronised).
-struct StageMaps {
-  std::vector<std::pair<void*, uint64_t>> m;
-  void release() {
-    for (auto& x : m) {
-      (void)hipHostUnregister(x.first);
-      munmap(x.first, x.second);
-    }
-    m.clear();
-  }
-  ~StageMaps() { release(); }
-};
-
-// Files of a stage that are DMA'd from their page-locked mappings instead of
-// being read (opt-in; like SF_FILE_INPLACE, a file truncated while its
-// registered mapping is being copied hangs the queues, so it is off unless
-// asked for).
-// being read into the pinned stage: none by default.  With the per-device
-// cache, the 8-thread pread stage beats per-file registration at every size
-// measured (scripts/map_min_probe.py: 16 MiB files 40 vs 23 GB/s, 64 MiB 46
-// vs 33, 128 MiB 45 vs 34).  SF_MAP_MIN_MIB=n maps files >= n MiB (A/B knob).
-// Files larger than a stage still take sf_index_file's in-place route.
-inline uint64_t map_min_bytes() {
-  const char* e = getenv("SF_MAP_MIN_MIB");
-  const long v = e ? atol(e) : -1;
-  return v >= 0 ? (uint64_t)v << 20 : ~0ull;
-}
-
-// mapped[k] = the k-th file of the stage is mapped + registered (at ptrs[k]).
-void map_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, StageMaps& maps,
-               std::vector<const uint8_t*>& ptrs) {
-  ptrs.assign(st.files.size(), nullptr);
-  const uint64_t map_min = map_min_bytes();
-  const char* nomm = getenv("SF_NO_MMAP");
-  if (nomm && atoi(nomm)) return;
-  const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
-  std::vector<unsigned char> res;
-  for (size_t k = 0; k < st.files.size(); k++) {
-    const uint64_t n = size[st.files[k]];
-    if (n < map_min) continue;
-    const int fd = open(paths[st.files[k]], O_RDONLY);
-    if (fd < 0) continue;  // the pread route reports the error
-    struct stat sb;
-    void* m = (fstat(fd, &sb) == 0 && (uint64_t)sb.st_size == n) ? mmap(nullptr, n, PROT_READ, MAP_SHARED, fd, 0)
-                                                                  : MAP_FAILED;
-    close(fd);
-    if (m == MAP_FAILED) continue;
-    res.resize(ceil_div(n, pg));
-    uint64_t resident = 0;
-    if (mincore(m, n, res.data()) == 0)
-      for (unsigned char r : res) resident += r & 1u;
-    if (resident * 10 >= res.size() * 9 && hipHostRegister(m, n, hipHostRegisterReadOnly) == hipSuccess) {
-      maps.m.push_back({m, n});
-      ptrs[k] = static_cast<const uint8_t*>(m);
-    } else {
-      (void)hipGetLastError();
-      munmap(m, n);
-    }
-  }
-}
-
 // Fill `dst` with the stage's files: (file, <=16 MiB slice) work items taken
-// by up to io_threads() threads from an atomic counter.
+// by up to io_threads() threads from an atomic counter.  Files are only read
+// (pread), never mapped and page-locked: a truncation under a registered
+// mapping hangs the GPU queues.
 int read_stage(const char* const* paths, const FileStage& st, const std::vector<uint64_t>& size, uint8_t* dst,
-               std::atomic<int64_t>& bad, const std::vector<const uint8_t*>& mapped) {
+               std::atomic<int64_t>& bad) {
   constexpr uint64_t kSlice = 16ull << 20;
   struct Item { uint32_t k; uint64_t a, b; };
   std::vector<Item> items;
   for (uint32_t k = 0; k < st.files.size(); k++) {
-    if (mapped[k]) continue;  // goes to the device straight from its mapping
     const uint64_t n = size[st.files[k]];
     for (uint64_t a = 0; a < n; a += kSlice) items.push_back({k, a, std::min(n, a + kSlice)});
   }
@@ -145,6 +80,7 @@ int read_stage(const char* const* paths, const FileStage& st, const std::vector<
       uint8_t* d = dst + st.desc[it.k].offset;
       for (uint64_t got = it.a; ok && got < it.b;) {
         const ssize_t r = pread(fd, d + got, it.b - got, (off_t)got);
+        if (r < 0 && errno == EINTR) continue;  // a signal (profiler, Python handler) is not a bad file
         if (r <= 0) ok = false;  // error, or EOF before the size stat() gave
         else got += (uint64_t)r;
       }
@@ -307,14 +243,6 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
     return SF_OK;
   };
   std::atomic<int64_t> bad{-1};
-  StageMaps maps[2];
-  std::vector<const uint8_t*> mptr;
-  struct SyncOnExit {  // destroyed before maps: no mapping is released under an in-flight copy
-    hipStream_t* s;
-    ~SyncOnExit() {
-      for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(s[i]);
-    }
-  } sync_on_exit{streams};
   for (size_t k = 0; k < stages.size() && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     const FileStage& st = stages[k];
@@ -325,31 +253,15 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
       if ((rc = harvest(k - 2)) != SF_OK) break;
       tr.lap(tr.harvest_ms);
     }
-    maps[b].release();  // stage k-2's copies are done (its event was waited for above)
-    map_stage(paths, st, size, maps[b], mptr);
-    rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad, mptr);
+    rc = read_stage(paths, st, size, static_cast<uint8_t*>(pin[b].p), bad);
     tr.lap(tr.read_ms);
     if (rc) break;
     hipStream_t s = streams[b];
-    // H2D: each mapped file from its mapping, every run of consecutive
-    // pread files from the pinned stage in one copy.
-    uint8_t* dd = static_cast<uint8_t*>(ddata[b].p);
-    const uint8_t* pp = static_cast<const uint8_t*>(pin[b].p);
-    for (size_t j = 0; j < st.files.size() && rc == SF_OK;) {
-      const uint64_t o = st.desc[j].offset;
-      if (mptr[j]) {
-        if (st.desc[j].len && hipMemcpyAsync(dd + o, mptr[j], st.desc[j].len, hipMemcpyHostToDevice, s) != hipSuccess)
-          rc = SF_ENODEV;
-        j++;
-        continue;
-      }
-      size_t e = j;
-      while (e < st.files.size() && !mptr[e]) e++;
-      const uint64_t end = e < st.files.size() ? st.desc[e].offset : st.bytes;
-      if (end > o && hipMemcpyAsync(dd + o, pp + o, end - o, hipMemcpyHostToDevice, s) != hipSuccess) rc = SF_ENODEV;
-      j = e;
+    // H2D: the whole stage in one copy
+    if (st.bytes && hipMemcpyAsync(ddata[b].p, pin[b].p, st.bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = SF_ENODEV;
+      break;
     }
-    if (rc) break;
     uint64_t nb = 0;
     if (dev_bh[k] && hipMemsetAsync(stat_dev(b), 0, sizeof(int), s) != hipSuccess) { rc = SF_ENODEV; break; }
     rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
@@ -369,7 +281,6 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
   for (int i = 0; i < 2; i++)
     if (hipStreamSynchronize(streams[i]) != hipSuccess && rc == SF_OK) rc = SF_ENODEV;
   tr.lap(tr.wait_ms);
-  for (int i = 0; i < 2; i++) maps[i].release();  // every copy has completed
   if (rc == SF_OK)
     for (size_t k = stages.size() >= 2 ? stages.size() - 2 : 0; k < stages.size() && rc == SF_OK; k++)
       rc = harvest(k);

@@ -9,9 +9,12 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/ioctl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+
+#include <string>
 
 #include <algorithm>
 #include <atomic>
@@ -48,12 +51,95 @@ bool locked_by_us(uintptr_t a, uintptr_t e) {  // caller holds g_lock_mu
   return false;
 }
 
+// PROCMAP_QUERY (Linux 6.11+, include/uapi/linux/fs.h): one ioctl on
+// /proc/self/maps answers "the first VMA at or after addr with these
+// properties".  Declared here: the image's kernel headers predate it.
+struct ProcmapQuery {
+  uint64_t size, query_flags, query_addr;
+  uint64_t vma_start, vma_end, vma_flags, vma_page_size, vma_offset, inode;
+  uint32_t dev_major, dev_minor, vma_name_size, build_id_size;
+  uint64_t vma_name_addr, build_id_addr;
+};
+constexpr uint64_t kQueryCoveringOrNext = 0x10, kQueryFileBacked = 0x20;
+constexpr unsigned long kProcmapQuery = _IOWR('f', 17, ProcmapQuery);
+
+// Is [a, e) private anonymous memory only (heap, anonymous mmap, stack)?
+// The in-place routes page-lock the caller's pages (hipHostRegister makes
+// them a GPU userptr).  For a file mapping -- and shared memory, which has a
+// file behind it too -- a concurrent truncation invalidates that userptr under
+// the copies in flight, and on MI355X the process's queues then never resumed
+// (tests/test_gpu_robustness.py).  Such ranges are never
+// page-locked: they go through the pinned stages.  The ioctl where the kernel
+// has it, else /proc/self/maps parsed.
+bool private_anonymous(uintptr_t a, uintptr_t e) {
+  const int fd = open("/proc/self/maps", O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  ProcmapQuery q{};
+  q.size = sizeof(q);
+  q.query_flags = kQueryCoveringOrNext | kQueryFileBacked;
+  q.query_addr = a;
+  if (ioctl(fd, kProcmapQuery, &q) == 0) {
+    close(fd);
+    return q.vma_start >= e;  // the first file-backed VMA at or after a starts past the range
+  }
+  if (errno == ENOENT) {  // no file-backed VMA at or after a
+    close(fd);
+    return true;
+  }
+  // Older kernel: scan the text.  A VMA overlapping [a, e) must be anonymous
+  // (inode 0, device 00:00) and private ('p').
+  std::string txt;
+  char buf[1 << 16];
+  for (ssize_t r; (r = read(fd, buf, sizeof(buf))) != 0;) {
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    txt.append(buf, (size_t)r);
+  }
+  close(fd);
+  bool covered = true;
+  for (size_t pos = 0; pos < txt.size();) {
+    size_t nl = txt.find('\n', pos);
+    if (nl == std::string::npos) nl = txt.size();
+    unsigned long lo = 0, hi = 0, off = 0, ino = 0;
+    unsigned maj = 0, mnr = 0;
+    char perms[8] = {0};
+    if (sscanf(txt.c_str() + pos, "%lx-%lx %7s %lx %x:%x %lu", &lo, &hi, perms, &off, &maj, &mnr, &ino) == 7 &&
+        lo < e && a < hi && (ino != 0 || maj != 0 || mnr != 0 || perms[3] != 'p'))
+      covered = false;
+    pos = nl + 1;
+  }
+  return covered;
+}
+
+// Memory the caller page-locked itself (hipHostMalloc, hipHostRegister):
+// copied from as it is.
+bool pinned_by_hip(uintptr_t a, uintptr_t e) {
+  for (uintptr_t p : {a, e - 1}) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, (const void*)p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 PageLock lock_pages(uintptr_t a, uintptr_t e) {
   std::lock_guard<std::mutex> lk(g_lock_mu);
   if (locked_by_us(a, e)) return kNotLocked;
+  if (!private_anonymous(a, e)) {
+    if (pinned_by_hip(a, e)) return kPinnedByCaller;
+    stat_add(S_NOT_ANON_REFUSED);
+    return kNotLocked;
+  }
   const hipError_t err = hipHostRegister((void*)a, e - a, hipHostRegisterReadOnly);
   if (err == hipSuccess) {
     g_locked.push_back({a, e});
+    stat_add(S_PAGES_LOCKED);
     return kLockedByUs;
   }
   (void)hipGetLastError();
@@ -81,19 +167,14 @@ struct PinBuf {
   ~PinBuf() { if (p) (void)hipHostFree(p); }
 };
 
-// Smallest host buffer / page-cache-resident file that sf_index_buffer /
-// sf_index_file copy in place (page-locked) instead of staging through the
-// pinned stages.  Per call, with the per-device set cached
-// (scripts/inplace_min_probe.py): a buffer gains in place from 1 MiB up
-// (7.6 vs 6.1 GB/s; 32 MiB: 45 vs 21); a file only from ~16 MiB (mapping and
-// locking page-cache pages loses to the 8-thread pread below 8 MiB: 4 MiB
-// 8.7 vs 10.3 GB/s; 32 MiB 24.3 vs 23.6).  SF_INPLACE_MIN_MIB overrides both
-// (A/B knob).
-inline uint64_t inplace_min_bytes(bool file) {
-  const char* e = getenv("SF_INPLACE_MIN_MIB");
-  const long v = e ? atol(e) : -1;
-  if (v >= 0) return (uint64_t)v << 20;
-  return file ? 16ull << 20 : 1ull << 20;
+// Smallest host buffer that sf_index_buffer / sf_index_buffer_blocks copy in
+// place (page-locked) instead of staging through the pinned stages.  Per call,
+// with the per-device set cached (scripts/inplace_min_probe.py): a buffer
+// gains in place from 1 MiB up (7.6 vs 6.1 GB/s; 32 MiB: 45 vs 21).
+// SF_INPLACE_MIN_MIB overrides it (A/B knob).
+inline uint64_t inplace_min_bytes() {
+  const int64_t v = knob(K_INPLACE_MIN_MIB);
+  return v >= 0 ? (uint64_t)v << 20 : 1ull << 20;
 }
 
 // Chunk of input handled per pipeline stage: a whole number of blocks, about
@@ -104,9 +185,9 @@ inline uint64_t stage_bytes(uint32_t bs) {
   return nb * bs;
 }
 
-// In-place route of sf_index_buffer / sf_index_file: the DMA engine reads the
-// caller's pages (or the page-cache pages of a mapped file) directly, no
-// staging memcpy.  Per ~256 MiB stage, on alternating streams: H2D, the
+// In-place route of sf_index_buffer: the DMA engine reads the caller's pages
+// directly, no staging memcpy.  Only private anonymous memory is page-locked
+// (lock_pages); a file mapping passed as a buffer takes the staged route.  Per ~256 MiB stage, on alternating streams: H2D, the
 // block kernel, D2H of the stage's digests.  The host overlaps the rest with
 // the PCIe link:
 //   - the pages are page-locked (hipHostRegister) one region ahead of the
@@ -118,22 +199,16 @@ inline uint64_t stage_bytes(uint32_t bs) {
 // k, and no page is registered twice.  A
 // region that cannot be registered after the first one switches the rest of
 // the stages to a pinned bounce buffer (memcpy, one stage at a time): slower,
-// same result.  For a mapped file (fd >= 0) the bounce buffer is filled
-// with pread from the fd, never by touching the mapping: a region that cannot
-// be page-locked is typically one past a concurrent truncation, and reading
-// the mapping there would raise SIGBUS; pread returns short instead, and the
-// call fails with SF_EIO (the reference's read() would see the short file).
-// Returns SF_ENOTSUP (nothing done) when the first region cannot be
-// registered, so the caller can take its staged route.
+// same result.  Returns SF_ENOTSUP (nothing done) when the first region cannot
+// be registered, so the caller can take its staged route.
 // SF_INPLACE_SERIAL=1 registers the whole range first and writes rows and
 // blocks_hash after the last stage (the previous form; A/B knob).
 int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* out, uint64_t cap,
-                         uint64_t* n_out, uint8_t* blocks_hash, int fd = -1) {
+                  uint64_t* n_out, uint8_t* blocks_hash) {
   const uint64_t nblocks = ceil_div(len, bs);
   if (n_out) *n_out = nblocks;
   if (nblocks > cap) return SF_ENOSPC;
-  const char* ser = getenv("SF_INPLACE_SERIAL");
-  const bool serial = ser && atoi(ser);
+  const bool serial = knob(K_INPLACE_SERIAL) != 0;
   const uint64_t stage = std::min<uint64_t>(stage_bytes(bs), len);
   const uint64_t nstages = ceil_div(len, stage);
   const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
@@ -165,15 +240,14 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
   };
   // (pages a concurrent call of ours locked are not the caller's pinning)
   const bool prepinned = pinned_at(data) && pinned_at(data + len - 1) && !range_locked_by_us(lo, hi);
-  const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to register
-  const long fail_k = fail_at ? atol(fail_at) : -1;
+  const int64_t fail_k = knob(K_TEST_INPLACE_FAIL_AT);  // test hook: region k "fails" to register
   auto reg = [&](uint64_t k) {
     const uintptr_t a = serial ? lo : edge(k), e = serial ? hi : edge(k + 1);
     // after one failure every later region stays pageable (a stage straddles
     // the page it shares with the previous region)
     if (e <= a) { regs.push_back({(void*)a, kEmpty}); return; }
     if (prepinned) { regs.push_back({(void*)a, kPinned}); return; }
-    if ((!regs.empty() && regs.back().second == kPageable) || (long)k == fail_k) {
+    if ((!regs.empty() && regs.back().second == kPageable) || (int64_t)k == fail_k) {
       regs.push_back({(void*)a, kPageable});
       return;
     }
@@ -216,18 +290,7 @@ int index_inplace(const uint8_t* data, uint64_t len, uint32_t bs, sf_block_sig* 
         if (hipStreamSynchronize(st[i]) != hipSuccess) rc = SF_ENODEV;
       if (rc != SF_OK) break;
       if (!bounce.p) SF_HIP(hipHostMalloc(&bounce.p, stage, hipHostMallocDefault));
-      if (fd >= 0) {
-        uint8_t* d = static_cast<uint8_t*>(bounce.p);
-        for (uint64_t got = 0; got < n && rc == SF_OK;) {
-          const ssize_t r = pread(fd, d + got, n - got, (off_t)(off + got));
-          if (r < 0 && errno == EINTR) continue;
-          if (r <= 0) rc = SF_EIO;  // error, or the file shrank under us
-          else got += (uint64_t)r;
-        }
-        if (rc != SF_OK) break;
-      } else {
-        memcpy(bounce.p, src, n);
-      }
+      memcpy(bounce.p, src, n);
       src = static_cast<const uint8_t*>(bounce.p);
     }
     // A copy must lie inside ONE registration: a stage that starts mid-page
@@ -303,8 +366,8 @@ static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks,
   uint64_t dl = 1;
   for (uint64_t v = last; v >= 10; v /= 10) dl++;
   const uint64_t msg = 33 + db;  // every message but the last
-  const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
-  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : kWireChunk);
+  const int64_t wc = knob(K_TEST_WIRE_CHUNK);  // messages per chunk (SF_TEST_WIRE_CHUNK test hook)
+  const uint64_t per = wc > 0 ? (uint64_t)wc : kWireChunk;
   const uint64_t nchunks = ceil_div(nb, per);
   const uint64_t cap = std::min(per, nb) * msg + (33 + dl);
   // Streams, events and the two chunk buffers (device + pinned) come from the
@@ -362,7 +425,7 @@ static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks,
 }
 
 // The FILE_BLOCK run of an explicit list streamed to fd: chunks of
-// SF_WIRE_CHUNK messages, each built by sf_wire_blocks_device (lengths, scan,
+// SF_TEST_WIRE_CHUNK messages (default 2^18), each built by sf_wire_blocks_device (lengths, scan,
 // scatter; it blocks until the chunk's size is known), copied back into a
 // pinned buffer and written while the next chunk is built.
 static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes, uint64_t n_blocks, int fd,
@@ -370,8 +433,8 @@ static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes
   if (n_written) *n_written = 0;
   if (n_blocks == 0) return SF_OK;
   if (!d_digests || !d_sizes || fd < 0) return SF_EINVAL;
-  const char* ce = getenv("SF_WIRE_CHUNK");  // messages per chunk (test knob)
-  const uint64_t per = std::max<uint64_t>(1, ce ? strtoull(ce, nullptr, 10) : kWireChunk);
+  const int64_t wc = knob(K_TEST_WIRE_CHUNK);  // messages per chunk (SF_TEST_WIRE_CHUNK test hook)
+  const uint64_t per = wc > 0 ? (uint64_t)wc : kWireChunk;
   const uint64_t nchunks = ceil_div(n_blocks, per);
   const uint64_t cap = std::min(per, n_blocks) * 43;  // 33 + at most 10 digits per message
   HostLease res;
@@ -437,8 +500,8 @@ namespace {
 // blocks_hash (src/index.rs:661-682), in order.  No device memory maps or
 // registers the caller's file: the host only ever reads it with read/pread.
 inline uint64_t file_stage_bytes(uint32_t bs) {
-  const char* se = getenv("SF_STREAM_STAGE_MIB");  // test knob: small stages exercise the pipeline
-  const uint64_t want = se ? std::max<uint64_t>(1, strtoull(se, nullptr, 10)) << 20 : (256ull << 20);
+  const int64_t sm = knob(K_TEST_STREAM_STAGE_MIB);  // test hook: small stages exercise the pipeline
+  const uint64_t want = sm > 0 ? (uint64_t)sm << 20 : (256ull << 20);
   return std::max<uint64_t>(1, want / bs) * bs;
 }
 
@@ -563,10 +626,7 @@ static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash)
 // before stage k is read, the kernel is asked to start fetching stage k+1
 // (POSIX_FADV_WILLNEED), so a file that is not in the page cache streams from
 // the disk while stage k is copied; for a resident file both are no-ops.
-inline bool fadvise_on() {
-  const char* e = getenv("SF_FADVISE");
-  return !e || atoi(e) != 0;
-}
+inline bool fadvise_on() { return knob(K_FADVISE) != 0; }
 
 // Bytes [base, base + len) of the file (base a multiple of bs: a shard of
 // one logical file); row offsets are file offsets.
@@ -651,7 +711,7 @@ constexpr uint64_t kListStageMaxBlocks = 1ull << 22;  // keeps a stage's list an
 template <typename FillFn>
 int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* sizes, uint64_t n, sf_block_sig* out,
                         uint8_t* blocks_hash, const uint8_t* direct = nullptr) {
-  const uint64_t target = file_stage_bytes(1);  // ~256 MiB (SF_STREAM_STAGE_MIB test knob)
+  const uint64_t target = file_stage_bytes(1);  // ~256 MiB (SF_TEST_STREAM_STAGE_MIB test hook)
   std::vector<ListStage> stages;
   uint64_t max_win = 0, max_blocks = 0;
   for (uint64_t i = 0; i < n;) {
@@ -673,8 +733,7 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
   const size_t nst = stages.size();
   bool inplace = direct != nullptr;
   if (inplace) {
-    const char* noreg = getenv("SF_NO_HOSTREG");
-    inplace = !(noreg && atoi(noreg)) && stages.back().w1 - stages[0].w0 >= inplace_min_bytes(false);
+    inplace = knob(K_NO_HOSTREG) == 0 && stages.back().w1 - stages[0].w0 >= inplace_min_bytes();
     for (size_t k = 0; k < nst && inplace; k++)
       inplace = stages[k].w1 - stages[k].w0 >= 2 * pg && (k == 0 || stages[k - 1].w1 <= stages[k].w0);
   }
@@ -694,10 +753,9 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
         if ((*r)[k] == kLocked) unlock_pages(e(k));
     }
   } unreg{&region, edge};
-  const char* fail_at = getenv("SF_INPLACE_FAIL_AT");  // test hook: region k "fails" to page-lock
-  const long fail_k = fail_at ? atol(fail_at) : -1;
+  const int64_t fail_k = knob(K_TEST_INPLACE_FAIL_AT);  // test hook: region k "fails" to page-lock
   auto lock_region = [&](size_t k) {
-    if ((!region.empty() && region.back() == kFailed) || (long)k == fail_k) { region.push_back(kFailed); return; }
+    if ((!region.empty() && region.back() == kFailed) || (int64_t)k == fail_k) { region.push_back(kFailed); return; }
     const PageLock pl = lock_pages(edge(k), edge(k + 1));
     region.push_back(pl == kLockedByUs ? kLocked : pl == kPinnedByCaller ? kPinned : kFailed);
   };
@@ -870,10 +928,9 @@ static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t bloc
   int rc = check_fixed_args(len, block_size);
   if (rc) return rc;
   if (len && (!data || !out)) return SF_EINVAL;
-  // Large buffers: page-lock in place (no staging memcpy); SF_NO_HOSTREG=1
-  // forces the staged path (A/B knob).
-  const char* noreg = getenv("SF_NO_HOSTREG");
-  if (len && len >= inplace_min_bytes(false) && !(noreg && atoi(noreg))) {
+  // Large buffers of private anonymous memory: page-locked in place (no
+  // staging memcpy); SF_NO_HOSTREG=1 forces the staged path (A/B knob).
+  if (len && len >= inplace_min_bytes() && knob(K_NO_HOSTREG) == 0) {
     rc = index_inplace(data, len, block_size, out, cap, n_out, nullptr);
     if (rc != SF_ENOTSUP) return rc;
   }
@@ -927,35 +984,12 @@ static int sf_index_file_body(const char* path, uint32_t block_size, sf_block_si
   if (n_out) *n_out = nb;
   if (nb > cap) { close(fd); return SF_ENOSPC; }
   if (nb && !out) { close(fd); return SF_EINVAL; }
-  // Opt-in (SF_FILE_INPLACE=1): a large file already in the page cache is
-  // mapped and the mapping page-locked in place (hipHostRegister), so the DMA
-  // engine reads the page-cache pages directly -- no pread copy (the in-place
-  // path of sf_index_buffer).  Not the default: a registered file mapping is
-  // a GPU userptr, and a concurrent truncation of the file invalidates it
-  // under the in-flight copies -- measured on MI355X, the process's queues
-  // then never resume and the call hangs (tests/test_gpu_robustness.py).  The
-  // default pread pipeline only ever reads the file, so a file that shrinks
-  // mid-call gives SF_EIO, like the short read the reference would see.
-  const char* inpl = getenv("SF_FILE_INPLACE");
-  if (len && len >= inplace_min_bytes(true) && inpl && atoi(inpl)) {
-    void* m = mmap(nullptr, len, PROT_READ, MAP_SHARED, fd, 0);
-    if (m != MAP_FAILED) {
-      const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
-      std::vector<unsigned char> res(ceil_div(len, pg));
-      uint64_t resident = 0;
-      if (mincore(m, len, res.data()) == 0)
-        for (unsigned char r : res) resident += r & 1u;
-      if (resident * 10 >= res.size() * 9) {
-        rc = index_inplace(static_cast<const uint8_t*>(m), len, block_size, out, cap, n_out, blocks_hash, fd);
-        if (rc != SF_ENOTSUP) {
-          munmap(m, len);
-          close(fd);
-          return rc;
-        }
-      }
-      munmap(m, len);
-    }
-  }
+  // The file is only ever read (pread into the pinned stages), never mapped
+  // and page-locked: a registered file mapping is a GPU userptr, and a
+  // concurrent truncation of the file invalidates it under the in-flight
+  // copies -- measured on MI355X, the process's queues then never resumed
+  // (DESIGN.md 6).  A file that shrinks mid-call gives SF_EIO, like the short
+  // read the reference would see.
   if (nb == 0) {
     close(fd);
     static const uint8_t none = 0;

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <system_error>
@@ -36,6 +37,29 @@
   } while (0)
 
 namespace sfi __attribute__((visibility("hidden"))) {
+
+// Environment knobs, read once when the library is loaded (sf_knobs.cpp);
+// the launch and copy paths read these slots, never the environment.
+// Order = kKnobDefs[] (names, defaults).
+enum Knob {
+  K_IO_THREADS, K_INPLACE_MIN_MIB, K_INPLACE_SERIAL, K_FADVISE, K_NO_HOSTREG, K_TABLE_CLASS_BITS, K_TRACE,
+  K_TEST_INPLACE_FAIL_AT, K_TEST_WIRE_CHUNK, K_TEST_STREAM_STAGE_MIB, K_TEST_LAUNCH_MAX_BLOCKS, K_TEST_TABLE_SORT,
+  K_TEST_CHAIN_SPIN_LIMIT, K_TEST_STAGES, K_COUNT
+};
+struct KnobDef {
+  const char* env;
+  int64_t dflt;
+};
+extern const KnobDef kKnobDefs[K_COUNT];
+extern std::atomic<int64_t> g_knob[K_COUNT];
+inline int64_t knob(Knob k) { return g_knob[k].load(std::memory_order_relaxed); }
+
+// Counters of the routes the host entry points took (read by the tests
+// through sf_test_get_stat): pages the library page-locked, and ranges it
+// refused to page-lock because they are not private anonymous memory.
+enum Stat { S_PAGES_LOCKED, S_NOT_ANON_REFUSED, S_COUNT };
+extern std::atomic<int64_t> g_stat[S_COUNT];
+inline void stat_add(Stat s, int64_t v = 1) { g_stat[s].fetch_add(v, std::memory_order_relaxed); }
 
 // A C++ exception must not cross the extern "C" boundary: a C or Rust caller
 // would get std::terminate.  Every entry point that allocates, starts threads
@@ -220,14 +244,13 @@ class HostLease {
 };
 
 // Reader threads of the pread routes (sf_index_file, sf_index_files).
-// SF_IO_THREADS overrides the default of 16 (A/B knob).  With the stat phase
+// SF_IO_THREADS overrides the default of 16 (A/B knob, latched at load).  With the stat phase
 // parallel too, 16 readers beat 8 on many small files (10,537 files of
 // 0-200 KiB: 29.3 vs 24.1 GB/s, 12 and 24 no better; 8 MiB files flat at
 // 33-34 GB/s; profiles/r02/e2e/io_threads_8_12_16_24.log).
 inline unsigned io_threads() {
-  const char* e = getenv("SF_IO_THREADS");
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? (unsigned)std::min(v, 64) : 16u;
+  const int64_t v = knob(K_IO_THREADS);
+  return v > 0 ? (unsigned)std::min<int64_t>(v, 64) : 16u;
 }
 
 }  // namespace sfi

@@ -822,6 +822,166 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
   if (lane == 0) __hip_atomic_fetch_add(stage_done + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------- explicit lists at any offset
+// The reference's default blocks are content-defined (cdchunking ZPAQ,
+// src/index.rs:622-625): they start at any byte.  A wave of such blocks
+// still stages them through LDS by DMA (round 3):
+//   * step t stages kListPieces = 9 pieces of 16 B of every block,
+//     [a + 128t, a + 128t + 144) with a = off rounded down to 16 B, which
+//     holds the block's message bytes [off + 128t, off + 128t + 128) whatever
+//     off & 15 is (the 9th piece is the next step's first: an L2 hit);
+//   * a block's 9 pieces sit back to back in LDS (144-B slots), so one DMA
+//     wave-instruction reads ~7 blocks x 144 contiguous bytes;
+//   * each lane reads its 33 dwords from its own slot starting at dword
+//     (off & 15) >> 2 (LDS reads take per-lane addresses), and one v_perm per
+//     word shifts by off & 3 and byte-swaps at once (selector in a VGPR) --
+//     as many VALU as the aligned path's plain byte swap;
+//   * a lane's last chunks (the partial one with the 0x80 byte, and the
+//     length) are built from the same LDS words, so no lane ever issues its
+//     own global load; chunks past a lane's message are skipped (exec mask),
+//     which in a length-sorted wave costs ~1 chunk of 130.
+constexpr int kListPieces = 9;
+constexpr int kListSlotDw = kListPieces * 4;  // dwords per block slot
+
+template <int NP>
+__device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t span16, uint32_t step,
+                                             const uint32_t (&voff)[NP], uint4* wave_tile) {
+  const uint64_t toff = (uint64_t)step * 128u;
+  const uint64_t left = span16 > toff ? span16 - toff : 0;
+  const uint32_t nrec = __builtin_amdgcn_readfirstlane(left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left);
+  const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
+  __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
+}
+
+// Words of chunk c of a message of `size` bytes whose data words (already
+// big-endian) are in w: keep the rem = size - 64c data bytes, then the 0x80
+// byte, zeros, and the bit length if c is the last chunk (nch - 1).
+__device__ __forceinline__ void finish_chunk(uint32_t (&w)[16], uint32_t size, uint32_t c, uint32_t nch) {
+  const int rem = (int)size - (int)(c * 64u);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int v = rem - 4 * j;  // data bytes in word j
+    uint32_t x;
+    if (v >= 4) x = w[j];
+    else if (v > 0) x = (w[j] & (0xFFFFFFFFu << (32 - 8 * v))) | (0x80u << (24 - 8 * v));
+    else if (v == 0) x = 0x80000000u;
+    else x = 0u;
+    w[j] = x;
+  }
+  if (c + 1 == nch) {
+    w[14] = size >> 29;
+    w[15] = size << 3;
+  }
+}
+
+#ifndef SF_LIST_DW_READS
+#define SF_LIST_DW_READS 0  // 1: 16-B aligned pieces + per-lane dword reads at (off & 15) >> 2 (A/B)
+#endif
+// A lane's 33 message dwords of one step out of its LDS slot.
+__device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint32_t* my) {
+#pragma unroll
+  for (int m = 0; m < 33; ++m) d[m] = my[m];
+}
+__device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint4* myq) {
+#pragma unroll
+  for (int k = 0; k < kListPieces; ++k) {
+    const uint4 v = myq[k];
+    d[4 * k + 0] = v.x;
+    d[4 * k + 1] = v.y;
+    d[4 * k + 2] = v.z;
+    d[4 * k + 3] = v.w;
+  }
+}
+
+// Hash this lane's block (off, size) of an explicit list through 144-B LDS
+// slots; all 64 lanes enter together.  base = the wave's lowest block start
+// rounded down to 16 B; span = bytes from base to the wave's highest block
+// end (< 4 GiB); data 16-B aligned.  Reads only inside [base, base + span
+// rounded up to 16 B): past the span the DMA returns zeros; the up-to-15
+// bytes the rounding adds share a 16-B granule with the block's last byte.
+__device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
+                                               bool valid, uint64_t base, uint64_t span, uint4* __restrict__ wave_tile,
+                                               Sha1& st) {
+  const int lane = threadIdx.x & 63;
+  st.init();
+  const uint32_t nch = n_chunks(size);                 // compressions of this lane's message
+  const uint32_t mine = valid ? size / 64u : 0u;       // its whole data chunks
+  const uint32_t nsteps = wave_max_u32(valid ? (nch + 1u) / 2u : 0u);
+#if SF_LIST_DW_READS
+  const uint32_t rel = valid ? (uint32_t)((off & ~15ull) - base) : 0u;
+#else
+  const uint32_t rel = valid ? (uint32_t)((off & ~3ull) - base) : 0u;  // pieces start at the block's dword
+#endif
+  uint32_t voff[kListPieces];
+#pragma unroll
+  for (int j = 0; j < kListPieces; ++j) {
+    const int p = 64 * j + lane;  // piece p of the tile: block p / 9, piece p % 9
+    const uint32_t rel_b = (uint32_t)__shfl((int)rel, p / kListPieces, 64);
+    voff[j] = rel_b + 16u * (uint32_t)(p % kListPieces);
+  }
+#if SF_LIST_DW_READS
+  const uint32_t* my = reinterpret_cast<const uint32_t*>(wave_tile) + lane * kListSlotDw +
+                       ((uint32_t)(off >> 2) & 3u);
+#else
+  const uint4* myq = wave_tile + lane * kListPieces;  // 144-B slots: 9 quads, so 16 lanes' b128 reads hit 16 bank quads
+#endif
+  const uint32_t sel = 0x00010203u + ((uint32_t)off & 3u) * 0x01010101u;  // shift by off & 3, then byte swap
+  const uint8_t* span_ptr = data + base;
+#if SF_LIST_DW_READS
+#define LIST_SRC my
+#else
+#define LIST_SRC myq
+#endif
+#if SF_LIST_DW_READS
+  const uint64_t span16 = (span + 15u) & ~15ull;
+#else
+  const uint64_t span16 = (span + 3u) & ~3ull;  // range-checked per dword: a dword holding a block byte is read
+#endif
+  // Steps in which every lane has two whole data chunks run branch-free (one
+  // basic block per step: the scheduler interleaves the two compressions, as
+  // in the aligned path); only the wave's last steps test each lane.
+  const uint32_t nfast = wave_min_u32(valid ? mine / 2u : 0xFFFFFFFFu);
+  if (nsteps > 0) issue_pieces(span_ptr, span16, 0, voff, wave_tile);
+  uint32_t t = 0;
+  for (; t < nfast; ++t) {
+    uint32_t d[36];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    list_read(d, LIST_SRC);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nsteps) issue_pieces(span_ptr, span16, t + 1, voff, wave_tile);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(d[16 * ch + j + 1], d[16 * ch + j], sel);
+      st.compress(w);
+    }
+  }
+  for (; t < nsteps; ++t) {
+    uint32_t d[36];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    list_read(d, LIST_SRC);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nsteps) issue_pieces(span_ptr, span16, t + 1, voff, wave_tile);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const uint32_t c = 2 * t + ch;
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_perm(d[16 * ch + j + 1], d[16 * ch + j], sel);
+      if (c < nch) {
+        if (c >= mine) finish_chunk(w, size, c, nch);
+        st.compress(w);
+      }
+    }
+  }
+#undef LIST_SRC
+}
+
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
 // Used for content-defined boundaries, the reference KAT boundaries, ragged
 // many-file batches, and (over the digest table) per-file blocks_hash.
@@ -839,7 +999,8 @@ __global__ void __launch_bounds__(kThreads, 3)  // 3 waves/SIMD, as the fixed ke
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
                   int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order) {
-  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
+  constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
+  __shared__ uint4 smem[kWavesPerWG * kWaveTile];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
@@ -873,8 +1034,17 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 
   Sha1 st;
   Adler wk;
-  hash_wave<TILE, false, WEAK>(data, off, size, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, PadSchedule{},
-                               wk);
+  uint4* tile = smem + wid * kWaveTile;
+#ifndef SF_LIST_ALIGNED_TOO
+#define SF_LIST_ALIGNED_TOO 0  // 1: 16-B aligned waves take the 144-B slot path too (A/B)
+#endif
+  const uint64_t lo16 = lo & ~15ull;
+  const bool list_path = !WEAK && (SF_LIST_ALIGNED_TOO || !geo.lds_ok) &&
+                         ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && hi - lo16 < 0xF0000000ull;
+  if (list_path)
+    hash_wave_list(data, off, size, valid, lo16, hi - lo16, tile, st);
+  else
+    hash_wave<TILE, false, WEAK>(data, off, size, rel, valid, geo, tile, st, PadSchedule{}, wk);
   if (valid) {
     if (bad) {
       uint32_t* o = reinterpret_cast<uint32_t*>(digests + blk * 20);

@@ -33,3 +33,25 @@ def golden():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture
+def knobs():
+    """Set library knobs for one test and restore them after it.  The library
+    reads the environment once, when it is loaded (syncfast_amd/csrc/
+    sf_knobs.cpp), so tests set knobs through the test hook
+    (include/syncfast_amd_test.h), not with monkeypatch.setenv."""
+    from syncfast_amd import _lib
+    saved = {}
+
+    class Knobs:
+        def set(self, name, value):
+            old = _lib.set_knob(name, int(value))
+            saved.setdefault(name, old)
+
+        def get(self, name):
+            return _lib.get_knob(name)
+
+    yield Knobs()
+    for name, value in saved.items():
+        _lib.set_knob(name, value)

@@ -31,7 +31,8 @@ def test_self_launch_two_ranks():
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
-    assert line == {"launch_check": True, "n_gpus": 2, "ranks_seen": 2}
+    assert {k: line[k] for k in ("launch_check", "n_gpus", "ranks_seen")} == \
+        {"launch_check": True, "n_gpus": 2, "ranks_seen": 2}
     assert "launching 2 ranks" in r.stderr
 
 
@@ -40,6 +41,29 @@ def test_self_launch_three_ranks():
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     assert _last_json(r.stdout)["n_gpus"] == 3
+
+
+def test_multi_block_three_ranks():
+    """An N > 1 line carries a `multi` block (per-rank kernel time, gather
+    waits as receiving rank and as sender, rank-0-reported world size).  The
+    kernel needs a GPU, so on CPU the launch check builds the same block from
+    stand-in per-rank numbers (rank r reports r + 1 ms) over gloo, through
+    the same code (bench.multi_block) the GPU run uses."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--dist-backend", "gloo", "--shard-gib", "0.01",
+                        "--steps", "6", "--check-launch"], capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = _last_json(r.stdout)["multi"]
+    assert m["world"] == 3 and m["backend"] == "gloo"
+    assert m["kernel_ms"] == {"max": 3.0, "min": 1.0, "per_rank": [1.0, 2.0, 3.0]}
+    assert len(m["gather_wait_ms_as_root"]) == len(m["gather_wait_ms_as_sender"]) == 3
+    assert m["steps_as_root"] == [2, 2, 2]
+
+
+def test_dist_timeout_is_passed():
+    # a stuck collective must fail the run, not hang it: the process group
+    # is created with --dist-timeout (default 300 s)
+    src = open(BENCH).read()
+    assert src.count("timeout=tmo") == 2 and '"--dist-timeout", type=float, default=300.0' in src
 
 
 def test_world_size_mismatch_fails():

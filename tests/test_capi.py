@@ -16,8 +16,8 @@ from syncfast_amd import _lib, host
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "syncfast_amd.h")).read()
+def header_functions(header="syncfast_amd.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(sf_[a-z0-9_]+)\s*\(", src)))
 
@@ -29,6 +29,78 @@ def test_header_symbols_exported():
     assert sorted(_lib.EXPORTED) == names
     for n in names:
         assert hasattr(L, n), n
+    tnames = header_functions("syncfast_amd_test.h")
+    assert sorted(_lib.EXPORTED_TEST) == tnames
+    for n in tnames:
+        assert hasattr(L, n), n
+
+
+def test_every_include_header_is_checked():
+    assert sorted(os.listdir(os.path.join(ROOT, "include"))) == ["syncfast_amd.h", "syncfast_amd_test.h"]
+
+
+def _strip_tuning_blocks(src):
+    """Source text without the #ifdef SF_TUNING ... #endif regions (tuning
+    builds only; the shipped library is built without SF_TUNING)."""
+    out, depth = [], 0
+    for line in src.splitlines():
+        t = line.strip()
+        if depth:
+            if t.startswith("#if"):
+                depth += 1
+            elif t.startswith("#endif"):
+                depth -= 1
+            continue
+        if t.startswith("#ifdef SF_TUNING") or t.startswith("#if defined(SF_TUNING)"):
+            depth = 1
+            continue
+        out.append(line)
+    return "\n".join(out)
+
+
+def test_environment_read_only_at_load():
+    """Knobs are latched once when the library is loaded (sf_knobs.cpp): no
+    other translation unit of the shipped library calls getenv, so nothing on
+    a launch or copy path consults the environment."""
+    csrc = os.path.join(ROOT, "syncfast_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)):
+        if fn.endswith((".hip", ".hpp", ".cpp", ".h")) and fn != "sf_knobs.cpp":
+            src = _strip_tuning_blocks(open(os.path.join(csrc, fn)).read())
+            assert "getenv" not in src, fn
+
+
+def test_knobs_latched_at_load_and_set_by_the_hook(monkeypatch):
+    """A knob set in the environment after the library was loaded changes
+    nothing; sf_test_set_knob does.  Result- or error-changing hooks carry the
+    SF_TEST_ prefix; the old unprefixed names are gone."""
+    syncfast_amd.lib()
+    before = _lib.get_knob("SF_TEST_TABLE_SORT")
+    monkeypatch.setenv("SF_TEST_TABLE_SORT", "1" if before != 1 else "0")
+    assert _lib.get_knob("SF_TEST_TABLE_SORT") == before
+    old = _lib.set_knob("SF_TEST_TABLE_SORT", 1)
+    try:
+        assert old == before and _lib.get_knob("SF_TEST_TABLE_SORT") == 1
+    finally:
+        _lib.set_knob("SF_TEST_TABLE_SORT", before)
+    for gone in ("SF_TABLE_SORT", "SF_CHAIN_SPIN_LIMIT", "SF_LAUNCH_MAX_BLOCKS", "SF_INPLACE_FAIL_AT", "SF_STAGES",
+                 "SF_FILE_INPLACE", "SF_MAP_MIN_MIB"):
+        with pytest.raises(_lib.SfError):
+            _lib.get_knob(gone)
+    for name in ("SF_TEST_CHAIN_SPIN_LIMIT", "SF_TEST_LAUNCH_MAX_BLOCKS", "SF_TEST_INPLACE_FAIL_AT",
+                 "SF_TEST_STAGES", "SF_TEST_WIRE_CHUNK", "SF_TEST_STREAM_STAGE_MIB", "SF_IO_THREADS"):
+        _lib.get_knob(name)
+    assert _lib.get_stat("pages_locked") >= 0 and _lib.get_stat("not_anon_refused") >= 0
+
+
+def test_knobs_from_the_environment_at_load(tmp_path):
+    """The environment at load time sets the knobs (a fresh process)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from syncfast_amd import _lib; "
+            "print(_lib.get_knob('SF_TEST_TABLE_SORT'), _lib.get_knob('SF_IO_THREADS'))" % ROOT)
+    env = dict(os.environ, SF_TEST_TABLE_SORT="0", SF_IO_THREADS="7")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.split() == ["0", "7"]
 
 
 def test_version_and_errors():
@@ -228,18 +300,18 @@ def test_product_does_not_import_oracle():
                 assert "sf_oracle" not in src and "sfo_" not in src, fn
 
 
-def test_traffic_profile_is_for_these_kernels():
+def test_traffic_profile_is_for_this_kernel():
     # bench.py reports roofline.traffic only when profiles/traffic.json was
-    # measured on the same gfx950 code objects; this keeps the committed PMC
-    # pass in step with the kernels (refresh it after any kernel change:
-    # PROFILE=1 scripts/gpu_round.sh, then scripts/pmc_traffic.py)
+    # measured on the same machine code of the headline kernel; this keeps the
+    # committed PMC pass in step with it (refresh it after any change to that
+    # kernel: PROFILE=1 scripts/gpu_round.sh, then scripts/pmc_traffic.py)
     import json
-    from syncfast_amd._lib import code_object_sha256
-    h = code_object_sha256()
+    from syncfast_amd._lib import kernel_code_sha256
+    h = kernel_code_sha256()
     assert len(h) == 64
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
         tr = json.load(f)
-    assert tr["config2"]["code_object_sha256"] == h
+    assert tr["config2"]["kernel_code_sha256"] == h
 
 
 @pytest.mark.parametrize("n", [0, 1, 3276, 3277, 10_000])

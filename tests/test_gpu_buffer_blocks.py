@@ -3,7 +3,7 @@ form a Rust caller uses when it keeps the reference's own chunker
 (cdchunking ZPAQ, src/index.rs:622-625) on the host and hands the bytes and
 boundaries to the library: every digest and the blocks_hash in list order
 must equal the oracle's restatement of src/index.rs:621-682, across stage
-edges (SF_STREAM_STAGE_MIB shrinks the ~256 MiB stages), for overlapping and
+edges (SF_TEST_STREAM_STAGE_MIB shrinks the ~256 MiB stages), for overlapping and
 empty blocks, blocks larger than a stage, and lists long enough for the
 launcher's length sort (>= 2^17 blocks in one stage)."""
 import hashlib
@@ -26,8 +26,8 @@ KAT_BLOCKS_HASH = "84c25d78edcdb67631639c43604cf0149564f044"
 
 
 @pytest.fixture
-def small_stages(monkeypatch):
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", "1")
+def small_stages(knobs):
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", 1)
     yield
     host.release_cache()
 
@@ -149,17 +149,16 @@ def test_errors_leave_nothing_running(gpu):
     assert bh == hashlib.sha1(hashlib.sha1(data.tobytes()).digest()).digest()
 
 
-def test_stage_knob_does_not_change_results(gpu):
+def test_stage_knob_does_not_change_results(gpu, knobs):
     rng = np.random.default_rng(17)
     n = 6 << 20
     data = oracle.splitmix_bytes(n, 17)
     offs, sizes = _cdc_like(rng, n)
     a = host.index_buffer_blocks(data, offs, sizes)
-    os.environ["SF_STREAM_STAGE_MIB"] = "2"
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", 2)
     try:
         b = host.index_buffer_blocks(data, offs, sizes)
     finally:
-        del os.environ["SF_STREAM_STAGE_MIB"]
         host.release_cache()
     assert np.array_equal(a[0], b[0]) and a[1] == b[1]
 
@@ -206,16 +205,16 @@ def test_file_form_errors(gpu, tmp_path):
     assert e.value.errno == -SF_EIO
 
 
-@pytest.mark.parametrize("env", [{}, {"SF_NO_HOSTREG": "1"}, {"SF_INPLACE_FAIL_AT": "0"},
-                                 {"SF_INPLACE_FAIL_AT": "2"}])
-def test_in_place_and_staged_routes_agree(gpu, monkeypatch, env):
+@pytest.mark.parametrize("env", [{}, {"SF_NO_HOSTREG": 1}, {"SF_TEST_INPLACE_FAIL_AT": 0},
+                                 {"SF_TEST_INPLACE_FAIL_AT": 2}])
+def test_in_place_and_staged_routes_agree(gpu, env, knobs):
     """The buffer form copies a chunker's list in place (page-locked region by
     region) or through the pinned stages (SF_NO_HOSTREG=1, overlapping
-    windows, or a region that cannot be page-locked -- SF_INPLACE_FAIL_AT=k
+    windows, or a region that cannot be page-locked -- SF_TEST_INPLACE_FAIL_AT=k
     from region k on); every route gives the oracle's rows and blocks_hash."""
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", "1")
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", 1)
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        knobs.set(k, v)
     rng = np.random.default_rng(33)
     n = (6 << 20) + 4321
     raw = oracle.splitmix_bytes(n + 5, 33)

@@ -78,17 +78,14 @@ def test_index_files_matches_one_file_path(gpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("no_mmap", ["0", "1"])
 @pytest.mark.parametrize("stage", [0, 160 << 20])
-def test_index_files_large_mapped_and_pread(gpu, tmp_path, stage, no_mmap, monkeypatch):
-    """With SF_MAP_MIN_MIB=64, files >= 64 MiB that are in the page cache go
-    to the device straight from their mappings; smaller ones through the
-    pread stage.  Mixed in one stage (ragged route) and as equal files
-    (staged route); SF_NO_MMAP=1 forces pread for all (the default route).
-    Stages holding 64 MiB files take blocks_hash on the host (long runs).
-    Same rows either way."""
-    monkeypatch.setenv("SF_NO_MMAP", no_mmap)
-    monkeypatch.setenv("SF_MAP_MIN_MIB", "64")
+def test_index_files_large_files_pread_only(gpu, tmp_path, stage):
+    """Files of 64 MiB and more in the page cache: read with pread like every
+    other file (never mapped and page-locked: DESIGN.md 6), mixed in one stage
+    (ragged route) and as equal files (staged route).  Stages holding 64 MiB
+    files take blocks_hash on the host (long runs).  Nothing is page-locked."""
+    from syncfast_amd import _lib
+    locked = _lib.get_stat("pages_locked")
     sizes = [(64 << 20) + 4096, 100_000, (64 << 20) + 13, 0, 5 << 20, 77]
     paths = _write(tmp_path, sizes, 2100)
     rows, first, fh = host.index_files(paths, 4096, stage_bytes=stage)
@@ -97,6 +94,7 @@ def test_index_files_large_mapped_and_pread(gpu, tmp_path, stage, no_mmap, monke
     paths = _write(tmp_path, eq, 2200)
     rows, first, fh = host.index_files(paths, 4096, stage_bytes=stage)
     _check(paths, eq, 2200, 4096, rows, first, fh)
+    assert _lib.get_stat("pages_locked") == locked
 
 
 @pytest.mark.gpu

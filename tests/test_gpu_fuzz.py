@@ -101,13 +101,13 @@ def test_fuzz_batch(gpu, case):
 
 
 @pytest.mark.parametrize("case", range(60))
-def test_fuzz_host_routes(gpu, case, tmp_path, monkeypatch):
+def test_fuzz_host_routes(gpu, case, tmp_path, knobs):
     # one input through the buffer, file, fd and file-range entry points,
     # with small pipeline stages so stage edges land anywhere
     rng = np.random.default_rng(13_000 + case)
     bs = _bs(rng)
     n = _len(rng, bs)
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", str(int(rng.integers(1, 4))))
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", int(rng.integers(1, 4)))
     data = oracle.splitmix_bytes(n, 23_000 + case)
     offs, sizes, want = oracle.index_fixed(data, bs)
     bh_want = oracle.blocks_hash(want)
@@ -181,7 +181,7 @@ def test_fuzz_block_set(gpu, case):
 
 
 @pytest.mark.parametrize("case", range(60))
-def test_fuzz_explicit_list_host_routes(gpu, case, tmp_path, monkeypatch):
+def test_fuzz_explicit_list_host_routes(gpu, case, tmp_path, knobs):
     """A host chunker's list over host memory or a file (sf_index_buffer_blocks
     / sf_index_file_blocks): random block-size mixes (1-byte to 40 KiB blocks,
     gaps, overlaps on odd cases, empty blocks), odd buffer starts, random stage
@@ -209,9 +209,9 @@ def test_fuzz_explicit_list_host_routes(gpu, case, tmp_path, monkeypatch):
     sizes = np.asarray(sizes, np.uint32)
     order = np.argsort(offs, kind="stable")  # non-decreasing offsets, as a chunker gives
     offs, sizes = offs[order], sizes[order]
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", str(int(rng.choice([1, 2, 256]))))
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", int(rng.choice([1, 2, 256])))
     if rng.random() < 0.3:
-        monkeypatch.setenv("SF_NO_HOSTREG", "1")
+        knobs.set("SF_NO_HOSTREG", 1)
     want = oracle.index_blocks(data, offs, sizes)
     rows, bh = host.index_buffer_blocks(data, offs, sizes)
     assert np.array_equal(rows["sha1"], want) and bh == oracle.blocks_hash(want), (n, mean)

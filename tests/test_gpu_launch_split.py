@@ -4,7 +4,7 @@ HIP caps a launch at 2^32 - 1 work-items; the kernels run one lane per block,
 so a table of more than ~2^32 blocks (only reachable with tiny blocks, e.g.
 1-B blocks over 4 GiB or 16-B blocks over 64 GiB) is hashed as several
 launches over consecutive block ranges (sf_capi.hip, launch_max_blocks).
-SF_LAUNCH_MAX_BLOCKS lowers the piece size so the split runs at small sizes
+SF_TEST_LAUNCH_MAX_BLOCKS lowers the piece size so the split runs at small sizes
 through every launcher; one test crosses the real limit."""
 import numpy as np
 import pytest
@@ -18,8 +18,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def small_pieces(monkeypatch):
-    monkeypatch.setenv("SF_LAUNCH_MAX_BLOCKS", "48")
+def small_pieces(knobs):
+    knobs.set("SF_TEST_LAUNCH_MAX_BLOCKS", 48)
 
 
 @pytest.mark.parametrize("n,bs,shift", [(100_000, 64, 0), (77_777, 100, 3), (4096 * 300 + 5, 4096, 0),

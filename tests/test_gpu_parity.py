@@ -11,7 +11,7 @@ import pytest
 import torch
 
 import oracle
-from syncfast_amd import SfError, device, host
+from syncfast_amd import SfError, _lib, device, host
 
 pytestmark = pytest.mark.gpu
 
@@ -186,20 +186,20 @@ def test_index_file_end_to_end(gpu):
     assert bh == oracle.blocks_hash(want)
 
 
-@pytest.mark.parametrize("inplace", ["0", "1"])
-def test_index_file_large_both_routes(gpu, inplace, monkeypatch):
-    # default: the pread pipeline; SF_FILE_INPLACE=1 (opt-in): >= 16 MiB and
-    # in the page cache (just written) -> the mmap + hostRegister route.
-    # Same rows either way.
-    monkeypatch.setenv("SF_FILE_INPLACE", inplace)
+def test_index_file_large_never_page_locks(gpu):
+    # sf_index_file reads the file with pread into the pinned stages; it never
+    # maps and page-locks it (a truncation under a registered file mapping
+    # hung the GPU queues), even when it is in the page cache
     data = oracle.splitmix_bytes((96 << 20) + 4093, 95)
     with tempfile.NamedTemporaryFile(delete=False) as f:
         f.write(data.tobytes())
         path = f.name
+    locked = _lib.get_stat("pages_locked")
     try:
         rows, bh = host.index_file(path, 4096)
     finally:
         os.unlink(path)
+    assert _lib.get_stat("pages_locked") == locked
     offs, sizes, want = oracle.index_fixed(data, 4096)
     assert np.array_equal(rows["sha1"], want)
     assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
@@ -215,16 +215,16 @@ def inplace_case():
     return data, oracle.index_fixed_mt(data[3:], 4096, 8)
 
 
-@pytest.mark.parametrize("knob", [("", ""), ("SF_INPLACE_SERIAL", "1"), ("SF_INPLACE_FAIL_AT", "0"),
-                                  ("SF_INPLACE_FAIL_AT", "1"), ("SF_INPLACE_FAIL_AT", "2")])
-def test_index_buffer_inplace_routes(gpu, inplace_case, knob, monkeypatch):
+@pytest.mark.parametrize("knob", [("", ""), ("SF_INPLACE_SERIAL", "1"), ("SF_TEST_INPLACE_FAIL_AT", "0"),
+                                  ("SF_TEST_INPLACE_FAIL_AT", "1"), ("SF_TEST_INPLACE_FAIL_AT", "2")])
+def test_index_buffer_inplace_routes(gpu, inplace_case, knob, knobs):
     # sf_index_buffer page-locks the caller's pages one region ahead of the
     # copy that reads them; data[3:] is not page-aligned, so a stage reads the
     # last page of the previous region.  FAIL_AT=0: nothing can be locked
     # (staged route); FAIL_AT=k>0: regions >= k are copied through a bounce
     # buffer; SERIAL: whole range locked up front, rows after the last stage.
     if knob[0]:
-        monkeypatch.setenv(*knob)
+        knobs.set(knob[0], int(knob[1]))
     data, want = inplace_case
     n = data.size - 3
     rows = host.index_buffer(data[3:], 4096)
@@ -269,15 +269,9 @@ def test_host_cache_reuse_release_and_threads(gpu, inplace_case):
     assert np.array_equal(got[0], want) and np.array_equal(got[1], want_small)
 
 
-@pytest.mark.parametrize("route", ["pread", "inplace", "inplace_fail1"])
-def test_index_file_multi_stage(gpu, inplace_case, route, monkeypatch, tmp_path):
-    # a file of 2.4 stages, blocks_hash folded in stage by stage: the default
-    # pread pipeline; the opt-in in-place route (mapped, locked region by
-    # region); and the in-place route with regions >= 1 bounced via pread
-    if route != "pread":
-        monkeypatch.setenv("SF_FILE_INPLACE", "1")
-    if route == "inplace_fail1":
-        monkeypatch.setenv("SF_INPLACE_FAIL_AT", "1")
+def test_index_file_multi_stage(gpu, inplace_case, tmp_path):
+    # a file of 2.4 stages through the pread pipeline, blocks_hash folded in
+    # stage by stage
     data, want = inplace_case
     path = tmp_path / "f.bin"
     path.write_bytes(data[3:].tobytes())
@@ -287,11 +281,11 @@ def test_index_file_multi_stage(gpu, inplace_case, route, monkeypatch, tmp_path)
 
 
 @pytest.mark.parametrize("min_mib", ["", "1024"])
-def test_small_buffer_and_file_routes(gpu, min_mib, monkeypatch, tmp_path):
-    # defaults: buffers >= 1 MiB and page-cache files >= 16 MiB in place;
-    # SF_INPLACE_MIN_MIB=1024 stages both through the pinned buffers
+def test_small_buffer_and_file_routes(gpu, min_mib, knobs, tmp_path):
+    # defaults: buffers >= 1 MiB in place; SF_INPLACE_MIN_MIB=1024 stages them
+    # through the pinned buffers; files always take the pread pipeline
     if min_mib:
-        monkeypatch.setenv("SF_INPLACE_MIN_MIB", min_mib)
+        knobs.set("SF_INPLACE_MIN_MIB", int(min_mib))
     for n, seed in [((2 << 20) + 13, 97), ((20 << 20) + 4095, 98)]:
         data = oracle.splitmix_bytes(n + 5, seed)
         _, _, want = oracle.index_fixed(data[5:], 4096)
@@ -398,10 +392,10 @@ def test_concurrent_host_threads_own_streams(gpu):
 
 @pytest.mark.parametrize("n,bs,stage_mib", [((20 << 20) + 4095, 4096, "3"), ((7 << 20) + 1, 1000, "1"),
                                            ((6 << 20), 65536, "1"), (4096 * 3, 4096, "1")])
-def test_index_file_pread_small_stages(gpu, monkeypatch, tmp_path, n, bs, stage_mib):
+def test_index_file_pread_small_stages(gpu, knobs, tmp_path, n, bs, stage_mib):
     # the pread pipeline with small stages: many stage edges, rows and the
     # streaming blocks_hash emitted stage by stage in file order
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", stage_mib)
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", int(stage_mib))
     data = oracle.splitmix_bytes(n, 990 + bs % 97)
     path = tmp_path / "s.bin"
     data.tofile(path)

@@ -4,7 +4,7 @@
   (bounded) for block digests; a wait that gives up must surface as
   SF_ETIMEDOUT, never as an all-zero blocks_hash with rc = 0 (the reference
   never yields a hash it did not compute, src/index.rs:661-682).  Forced with
-  SF_CHAIN_SPIN_LIMIT=0 (one poll per wait; test knob).
+  SF_TEST_CHAIN_SPIN_LIMIT=0 (one poll per wait; test hook).
 - Batches too wide for the fused launch's chain workgroups to stay below the
   resident capacity, and callers without a status word, take the non-waiting
   path: correct hashes even with the spin limit at 0.
@@ -33,8 +33,8 @@ def _equal_batch(gpu, nfiles, nbf, bs, seed):
     return data, t, files
 
 
-def test_staged_chain_timeout_is_an_error(gpu, monkeypatch):
-    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+def test_staged_chain_timeout_is_an_error(gpu, knobs):
+    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
     _, t, files = _equal_batch(gpu, 64, 1024, 4096, 501)  # 256 MiB: stage 0 cannot be done at the first poll
     with pytest.raises(SfError) as e:
         device.index_device_batch(t, files, 4096)
@@ -55,7 +55,7 @@ def test_staged_default_spin_limit_is_green(gpu):
     assert bytes(fh.cpu().numpy()[63]) == oracle.blocks_hash(want[63 * 1024:])
 
 
-def test_index_files_reports_chain_timeout(gpu, monkeypatch, tmp_path):
+def test_index_files_reports_chain_timeout(gpu, tmp_path, knobs):
     # sf_index_files reads each stage's device status back: SF_ETIMEDOUT
     # from the blocks_hash lanes of a stage fails the call
     paths = []
@@ -66,16 +66,16 @@ def test_index_files_reports_chain_timeout(gpu, monkeypatch, tmp_path):
     rows, first, fh = host.index_files(paths, 4096)  # green first
     want = oracle.index_fixed(np.fromfile(paths[5], np.uint8), 4096)[2]
     assert bytes(fh[5]) == oracle.blocks_hash(want)
-    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
     with pytest.raises(SfError) as e:
         host.index_files(paths, 4096)
     assert e.value.code == SF_ETIMEDOUT
 
 
-def test_null_status_takes_nonwaiting_path(gpu, monkeypatch):
+def test_null_status_takes_nonwaiting_path(gpu, knobs):
     # no status word: the batch runs block kernel + chain kernel (no waits),
     # so even a zero spin limit gives the right hashes
-    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
     nfiles, nbf, bs = 64, 1024, 4096
     data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 503)
     descs = (FileDesc * nfiles)(*[FileDesc(o, ln) for o, ln in files])
@@ -93,10 +93,10 @@ def test_null_status_takes_nonwaiting_path(gpu, monkeypatch):
         assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
 
 
-def test_wide_batch_keeps_chains_below_residency(gpu, monkeypatch):
+def test_wide_batch_keeps_chains_below_residency(gpu, knobs):
     # 70,000 equal files: more chain workgroups (274) than CUs (256) -> the
     # non-waiting path; with the spin limit at 0 a fused launch would time out
-    monkeypatch.setenv("SF_CHAIN_SPIN_LIMIT", "0")
+    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
     nfiles, nbf, bs = 70_000, 128, 64
     data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 504)
     dig, _, fh = device.index_device_batch(t, files, bs)
@@ -111,9 +111,10 @@ def test_wide_batch_keeps_chains_below_residency(gpu, monkeypatch):
 def test_truncated_while_indexed_no_hang(gpu, tmp_path):
     # the default file route only reads the file (pread into pinned stages):
     # a concurrent truncation gives SF_EIO (short read) or a complete result,
-    # never a hang or SIGBUS.  (The opt-in SF_FILE_INPLACE route registers the
-    # mapping with the GPU; truncating it mid-copy hangs the queues, which is
-    # why it is not the default -- DESIGN.md section 6.)
+    # never a hang or SIGBUS.  (A route that registered the file's mapping
+    # with the GPU hung the queues when the file was truncated mid-copy; no
+    # route of the library page-locks file-backed memory any more -- DESIGN.md
+    # section 6, test_file_mapping_buffer_is_staged_not_page_locked.)
     size, bs = 768 << 20, 4096
     data = oracle.splitmix_bytes(size, 505)
     p = tmp_path / "shrinking"
@@ -133,6 +134,56 @@ def test_truncated_while_indexed_no_hang(gpu, tmp_path):
         finally:
             cut.join()
     assert all(o[0] in ("ok", -5) for o in outcomes), outcomes
+
+
+@pytest.mark.parametrize("form", ["fixed", "list"])
+def test_file_mapping_buffer_is_staged_not_page_locked(gpu, tmp_path, form):
+    """A caller's MAP_SHARED file mapping (Rust's memmap pattern) handed to
+    sf_index_buffer / sf_index_buffer_blocks is never page-locked (a GPU
+    userptr over a file that can be truncated under the copies hung the
+    queues): the library sees it is not private anonymous memory, copies it
+    through the pinned stages, and the rows are the oracle's.  An anonymous
+    buffer of the same bytes is page-locked in place (the counter moves), so
+    the test tells the routes apart."""
+    import mmap
+    from syncfast_amd import _lib
+    n = (40 << 20) + 4093
+    data = oracle.splitmix_bytes(n, 507)
+    p = tmp_path / "mapped.bin"
+    data.tofile(p)
+    rng = np.random.default_rng(507)
+    if form == "list":
+        sizes = np.minimum(32768, np.maximum(1, rng.geometric(1 / 8192, n // 4096))).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        keep = offs + sizes <= n
+        offs, sizes = offs[keep], sizes[keep]
+        want = oracle.index_blocks(data, offs, sizes)
+    else:
+        want = oracle.index_fixed(data, 4096)[2]
+
+    def run(buf):
+        if form == "list":
+            rows, bh = host.index_buffer_blocks(buf, offs, sizes)
+            assert bh == oracle.blocks_hash(want)
+            return rows
+        return host.index_buffer(buf, 4096)
+
+    with open(p, "rb") as f:
+        mm = mmap.mmap(f.fileno(), n, mmap.MAP_SHARED, mmap.PROT_READ)
+    locked, refused = _lib.get_stat("pages_locked"), _lib.get_stat("not_anon_refused")
+    view = np.frombuffer(mm, np.uint8)
+    try:
+        rows = run(view)
+    finally:
+        del view  # the array's buffer export must go before the mapping closes
+        mm.close()
+    assert np.array_equal(rows["sha1"], want)
+    assert _lib.get_stat("pages_locked") == locked, "a file mapping was page-locked"
+    assert _lib.get_stat("not_anon_refused") > refused
+    anon = data.copy()
+    locked = _lib.get_stat("pages_locked")
+    assert np.array_equal(run(anon)["sha1"], want)
+    assert _lib.get_stat("pages_locked") > locked  # the anonymous buffer took the in-place route
 
 
 def test_index_file_retries_when_the_file_grew(gpu, monkeypatch, tmp_path):

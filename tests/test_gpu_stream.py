@@ -4,7 +4,7 @@ The reference's index_file streams whatever File::open accepts -- a FIFO, a
 character device (src/index.rs:615,625).  sf_index_file takes such a path
 directly (rows within cap), and sf_index_fd reads any descriptor to EOF into
 a library-grown row buffer.  Rows and blocks_hash must equal the oracle's
-for the same bytes, across stage boundaries (SF_STREAM_STAGE_MIB=1 makes the
+for the same bytes, across stage boundaries (SF_TEST_STREAM_STAGE_MIB=1 makes the
 stages small so a few MiB cross several)."""
 import ctypes
 import os
@@ -46,9 +46,9 @@ def _check(rows, bh, data, bs):
 @pytest.mark.parametrize("n,bs,stage_mib", [(0, 4096, ""), (1, 4096, ""), (3 * 4096 + 1234, 4096, ""),
                                            ((5 << 20) + 777, 4096, "1"), ((3 << 20) + 1, 65536, "1"),
                                            ((2 << 20), 1000, "1"), (40 << 20, 4096, "")])
-def test_index_fd_pipe(gpu, monkeypatch, n, bs, stage_mib):
+def test_index_fd_pipe(gpu, n, bs, stage_mib, knobs):
     if stage_mib:
-        monkeypatch.setenv("SF_STREAM_STAGE_MIB", stage_mib)
+        knobs.set("SF_TEST_STREAM_STAGE_MIB", int(stage_mib))
     data = oracle.splitmix_bytes(n, 700 + n % 97)
     r, w = os.pipe()
     th = _writer(w, data.tobytes())
@@ -60,8 +60,8 @@ def test_index_fd_pipe(gpu, monkeypatch, n, bs, stage_mib):
     _check(rows, bh, data, bs)
 
 
-def test_sf_index_file_on_fifo(gpu, monkeypatch, tmp_path):
-    monkeypatch.setenv("SF_STREAM_STAGE_MIB", "1")
+def test_sf_index_file_on_fifo(gpu, tmp_path, knobs):
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", 1)
     fifo = tmp_path / "fifo"
     os.mkfifo(fifo)
     bs = 4096

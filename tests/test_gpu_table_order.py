@@ -5,7 +5,7 @@ The launcher sorts a list of >= 2^17 blocks by compression count, largest
 first, so each wave's 64 blocks are about the same length; every digest must
 still land at its block's own index, bit-identical to the oracle
 (src/index.rs:621-647 restated) and to the list-order launch.
-SF_TABLE_SORT=1 forces the sorted launch on small lists, SF_TABLE_SORT=0 the
+SF_TEST_TABLE_SORT=1 forces the sorted launch on small lists, SF_TEST_TABLE_SORT=0 the
 list order."""
 import numpy as np
 import pytest
@@ -39,7 +39,7 @@ def _cdc_like(rng, n, mean=8192, cap=32768):
 
 
 @pytest.mark.parametrize("case", range(60))
-def test_sorted_explicit_blocks_fuzz(gpu, case, monkeypatch):
+def test_sorted_explicit_blocks_fuzz(gpu, case, knobs):
     # random, overlapping, unsorted, empty and tiny-to-70 KB blocks, any
     # alignment of the data pointer: forced sort, then list order
     rng = np.random.default_rng(31_000 + case)
@@ -52,29 +52,29 @@ def test_sorted_explicit_blocks_fuzz(gpu, case, monkeypatch):
     to, tz = torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu)
     want = oracle.index_blocks(data, offs, sizes)
     for mode in ("1", "0"):
-        monkeypatch.setenv("SF_TABLE_SORT", mode)
+        knobs.set("SF_TEST_TABLE_SORT", int(mode))
         got = device.index_device_blocks(t, to, tz).cpu().numpy()
         assert np.array_equal(got, want), (mode, n, m)
 
 
 @pytest.mark.parametrize("case", range(12))
-def test_sorted_cdc_like_lists(gpu, case, monkeypatch):
+def test_sorted_cdc_like_lists(gpu, case, knobs):
     rng = np.random.default_rng(32_000 + case)
     n = int(rng.integers(1, 24 << 20))
     data = oracle.splitmix_bytes(n, 42_000 + case)
     offs, sizes = _cdc_like(rng, n)
     assert offs[-1] + sizes[-1] == n
     t = _dev(data, gpu, int(rng.integers(0, 16)))
-    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    knobs.set("SF_TEST_TABLE_SORT", 1)
     got = device.index_device_blocks(t, torch.from_numpy(offs).to(gpu),
                                      torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes)), (n, offs.size)
 
 
-def test_sorted_out_of_range_blocks(gpu, monkeypatch):
+def test_sorted_out_of_range_blocks(gpu, knobs):
     # blocks outside the buffer sort like any other (by their claimed size)
     # and still report SF_ERANGE with a zero digest at their own index
-    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    knobs.set("SF_TEST_TABLE_SORT", 1)
     rng = np.random.default_rng(33_000)
     n = 1 << 20
     data = oracle.splitmix_bytes(n, 43_000)
@@ -95,8 +95,8 @@ def test_sorted_out_of_range_blocks(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("case", range(6))
-def test_sorted_weak_blocks(gpu, case, monkeypatch):
-    monkeypatch.setenv("SF_TABLE_SORT", "1")
+def test_sorted_weak_blocks(gpu, case, knobs):
+    knobs.set("SF_TEST_TABLE_SORT", 1)
     rng = np.random.default_rng(34_000 + case)
     n = int(rng.integers(1, 6 << 20))
     data = oracle.splitmix_bytes(n, 44_000 + case)
@@ -109,10 +109,10 @@ def test_sorted_weak_blocks(gpu, case, monkeypatch):
 
 
 @pytest.mark.parametrize("case", range(20))
-def test_sorted_ragged_batch(gpu, case, monkeypatch):
+def test_sorted_ragged_batch(gpu, case, knobs):
     # ragged many-file batches: the block table and the per-file blocks_hash
     # table (one lane per file over runs of different lengths) both sorted
-    monkeypatch.setenv("SF_TABLE_SORT", "1")
+    knobs.set("SF_TEST_TABLE_SORT", 1)
     rng = np.random.default_rng(35_000 + case)
     bs = int(rng.choice([64, 100, 4096, 4097, 65536]))
     nf = int(rng.integers(1, 200))
@@ -131,10 +131,10 @@ def test_sorted_ragged_batch(gpu, case, monkeypatch):
         assert bytes(fh[k]) == oracle.blocks_hash(want), (k, ln, bs)
 
 
-def test_sorted_with_launch_split(gpu, monkeypatch):
+def test_sorted_with_launch_split(gpu, knobs):
     # a list larger than one launch: each piece sorted on its own
-    monkeypatch.setenv("SF_TABLE_SORT", "1")
-    monkeypatch.setenv("SF_LAUNCH_MAX_BLOCKS", "48")
+    knobs.set("SF_TEST_TABLE_SORT", 1)
+    knobs.set("SF_TEST_LAUNCH_MAX_BLOCKS", 48)
     rng = np.random.default_rng(36_000)
     n = 3 << 20
     data = oracle.splitmix_bytes(n, 46_000)
@@ -144,10 +144,10 @@ def test_sorted_with_launch_split(gpu, monkeypatch):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
 
 
-def test_default_sort_large_cdc_list(gpu, monkeypatch):
+def test_default_sort_large_cdc_list(gpu, knobs):
     # >= 2^17 blocks: the launcher sorts by itself; every digest equals the
     # list-order launch and the oracle
-    monkeypatch.delenv("SF_TABLE_SORT", raising=False)
+    knobs.set("SF_TEST_TABLE_SORT", -1)
     rng = np.random.default_rng(37_000)
     n = 1 << 30
     data = oracle.splitmix_bytes(n, 47_000)
@@ -156,6 +156,6 @@ def test_default_sort_large_cdc_list(gpu, monkeypatch):
     t = _dev(data, gpu, 5)
     to, tz = torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu)
     got = device.index_device_blocks(t, to, tz).cpu().numpy()
-    monkeypatch.setenv("SF_TABLE_SORT", "0")
+    knobs.set("SF_TEST_TABLE_SORT", 0)
     assert np.array_equal(got, device.index_device_blocks(t, to, tz).cpu().numpy())
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))

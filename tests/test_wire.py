@@ -90,11 +90,11 @@ def test_file_blocks_device_matches_write_message(gpu, n, bs):
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunk", ["1", "7", "1000", "0"])
 @pytest.mark.parametrize("n,bs", [(4096 * 2500 + 7, 4096), (999, 100), (4096, 4096)])
-def test_file_blocks_to_fd_streams_the_same_bytes(gpu, tmp_path, monkeypatch, n, bs, chunk):
-    # the streamed writer (chunks of SF_WIRE_CHUNK messages, double-buffered
+def test_file_blocks_to_fd_streams_the_same_bytes(gpu, tmp_path, n, bs, chunk, knobs):
+    # the streamed writer (chunks of SF_TEST_WIRE_CHUNK messages, double-buffered
     # D2H, in-order writes) produces exactly the device-built run
     if chunk != "0":
-        monkeypatch.setenv("SF_WIRE_CHUNK", chunk)
+        knobs.set("SF_TEST_WIRE_CHUNK", int(chunk))
     data = oracle.splitmix_bytes(n, n + 1)
     t = torch.from_numpy(data.copy()).to(gpu)
     dig = device.index_device(t, bs)
@@ -193,9 +193,9 @@ def test_blocks_device_equals_fixed_form_and_parses_back(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunk", ["1", "7", "1000", "0"])
-def test_blocks_to_fd_streams_the_device_run(gpu, tmp_path, monkeypatch, chunk):
+def test_blocks_to_fd_streams_the_device_run(gpu, tmp_path, chunk, knobs):
     if chunk != "0":
-        monkeypatch.setenv("SF_WIRE_CHUNK", chunk)
+        knobs.set("SF_TEST_WIRE_CHUNK", int(chunk))
     rng = np.random.default_rng(int(chunk) + 3)
     n = 20_000 if chunk != "1" else 700
     dig = torch.from_numpy(rng.integers(0, 256, (n, 20), dtype=np.uint8)).to(gpu)
