@@ -425,9 +425,10 @@ static int sf_wire_file_blocks_fd_body(const void* d_digests, uint64_t n_blocks,
 }
 
 // The FILE_BLOCK run of an explicit list streamed to fd: chunks of
-// SF_TEST_WIRE_CHUNK messages (default 2^18), each built by sf_wire_blocks_device (lengths, scan,
-// scatter; it blocks until the chunk's size is known), copied back into a
-// pinned buffer and written while the next chunk is built.
+// SF_TEST_WIRE_CHUNK messages (default 2^18).  The whole run is planned once
+// (message lengths, one scan, every chunk's end offset read back in one copy:
+// the only wait before the chunks), then chunk k is built on the device and
+// copied back while the host writes chunk k-2 -- no per-chunk host stall.
 static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes, uint64_t n_blocks, int fd,
                                   uint64_t* n_written, void* stream) {
   if (n_written) *n_written = 0;
@@ -436,23 +437,37 @@ static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes
   const int64_t wc = knob(K_TEST_WIRE_CHUNK);  // messages per chunk (SF_TEST_WIRE_CHUNK test hook)
   const uint64_t per = wc > 0 ? (uint64_t)wc : kWireChunk;
   const uint64_t nchunks = ceil_div(n_blocks, per);
-  const uint64_t cap = std::min(per, n_blocks) * 43;  // 33 + at most 10 digits per message
+  hipStream_t cs = as_stream(stream);  // digests and sizes are produced on the caller's stream
+  uint64_t* ends = nullptr;
+  int rc = wire_plan(d_sizes, n_blocks, &ends, cs);
+  if (rc != SF_OK) return rc;
+  struct FreeEnds {
+    uint64_t* p;
+    hipStream_t s;
+    ~FreeEnds() { (void)hipFreeAsync(p, s); }
+  } free_ends{ends, cs};
+  std::vector<uint64_t> cend(nchunks);
+  uint64_t* d_cend = nullptr;
+  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cend), nchunks * 8, cs));
+  if ((rc = wire_chunk_ends(ends, n_blocks, per, d_cend, cs)) == SF_OK &&
+      (hipMemcpyAsync(cend.data(), d_cend, nchunks * 8, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+       hipStreamSynchronize(cs) != hipSuccess))
+    rc = SF_ENODEV;
+  (void)hipFreeAsync(d_cend, cs);
+  if (rc != SF_OK) return rc;
+  uint64_t cap = 1;
+  for (uint64_t k = 0; k < nchunks; k++) cap = std::max(cap, cend[k] - (k ? cend[k - 1] : 0));
   HostLease res;
   hipStream_t* st;
   hipEvent_t* ev;
   void *dout[2], *pin[2];
-  hipEvent_t ready = nullptr;
   uint64_t bytes_of[2] = {0, 0};
-  int rc = res.streams(st, ev);
+  rc = res.streams(st, ev);
   for (int i = 0; i < 2 && rc == SF_OK; i++) {
     rc = res.dev(i, cap, &dout[i]);
     if (rc == SF_OK) rc = res.pin(i, cap, &pin[i]);
   }
-  if (rc != SF_OK) return rc;
-  SF_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-  if (hipEventRecord(ready, as_stream(stream)) != hipSuccess ||  // digests and sizes are produced on the caller's stream
-      hipStreamWaitEvent(st[0], ready, 0) != hipSuccess || hipStreamWaitEvent(st[1], ready, 0) != hipSuccess)
-    rc = SF_ENODEV;
+  if (rc != SF_OK) return rc;  // (the plan is complete: cs was synchronised above)
   uint64_t written = 0;
   auto flush = [&](int b) {
     if (hipEventSynchronize(ev[b]) != hipSuccess) return SF_ENODEV;
@@ -469,19 +484,17 @@ static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes
   for (uint64_t k = 0; k < nchunks && rc == SF_OK; k++) {
     const int b = (int)(k & 1);
     if (k >= 2 && (rc = flush(b)) != SF_OK) break;
-    const uint64_t i0 = k * per, cnt = std::min(per, n_blocks - i0);
-    uint64_t bytes = 0;
-    if ((rc = sf_wire_blocks_device(static_cast<const uint8_t*>(d_digests) + i0 * 20, d_sizes + i0, cnt, dout[b], cap,
-                                    &bytes, st[b])) != SF_OK)
+    const uint64_t i0 = k * per, cnt = std::min(per, n_blocks - i0), base = k ? cend[k - 1] : 0;
+    bytes_of[b] = cend[k] - base;
+    if ((rc = wire_build(static_cast<const uint8_t*>(d_digests), d_sizes, ends, i0, cnt, base,
+                         static_cast<uint8_t*>(dout[b]), st[b])) != SF_OK)
       break;
-    bytes_of[b] = bytes;
-    if (hipMemcpyAsync(pin[b], dout[b], bytes, hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
+    if (hipMemcpyAsync(pin[b], dout[b], bytes_of[b], hipMemcpyDeviceToHost, st[b]) != hipSuccess ||
         hipEventRecord(ev[b], st[b]) != hipSuccess)
       rc = SF_ENODEV;
   }
   for (uint64_t k = nchunks >= 2 ? nchunks - 2 : 0; k < nchunks && rc == SF_OK; k++) rc = flush((int)(k & 1));
-  for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(st[i]);
-  (void)hipEventDestroy(ready);
+  for (int i = 0; i < 2; i++) (void)hipStreamSynchronize(st[i]);  // before the plan is freed on cs
   if (n_written) *n_written = written;
   return rc;
 }

@@ -120,6 +120,14 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
                  uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr);
 int launch_wire(const uint8_t* d_digests, uint64_t n, uint32_t bs, uint32_t last, uint8_t* d_out,
                 hipStream_t stream);
+// FILE_BLOCK runs of explicit lists (sf_wire.hip): end offsets of every
+// message (stream-ordered allocation, hipFreeAsync on s), the end offset of
+// every chunk of `per` messages, and messages [first, first + cnt) written
+// from the start of d_out (base = end offset of message first - 1).
+int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_t s);
+int wire_chunk_ends(const uint64_t* d_ends, uint64_t n, uint64_t per, uint64_t* d_chunk_ends, hipStream_t s);
+int wire_build(const uint8_t* d_digests, const uint32_t* d_sizes, const uint64_t* d_ends, uint64_t first,
+               uint64_t cnt, uint64_t base, uint8_t* d_out, hipStream_t s);
 
 // Per-device resources of the host-memory entry points (streams, events,
 // device stage buffers, digest table, pinned stages), kept between calls:

@@ -843,6 +843,13 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
 constexpr int kListPieces = 9;
 constexpr int kListSlotDw = kListPieces * 4;  // dwords per block slot
 
+// Cache policy of the slot DMA: the default (0), not the aligned path's nt.
+// A step's 9th piece and the next step's 1st lie in the same 128-B line; with
+// nt the L2 did not keep that line between the two steps and HBM delivered
+// it twice (FETCH_SIZE 1.95x the algorithmic bytes, profiles/r03/).
+#ifndef SF_LIST_LOAD_AUX
+#define SF_LIST_LOAD_AUX 0
+#endif
 template <int NP>
 __device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t span16, uint32_t step,
                                              const uint32_t (&voff)[NP], uint4* wave_tile) {
@@ -854,7 +861,8 @@ __device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t s
       __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
 #pragma unroll
   for (int j = 0; j < NP; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0,
+                                             SF_LIST_LOAD_AUX);
 }
 
 // Words of chunk c of a message of `size` bytes whose data words (already
@@ -1079,6 +1087,67 @@ table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __re
   if (i >= n) return;
   keys[i] = length_class(n_chunks(sizes[i]), mbits);
   idx[i] = (uint32_t)i;
+}
+
+// Bucketing by length class without a radix sort (the launcher's default):
+// a histogram of the classes, one workgroup turns it into bucket starts
+// (longest class first), and every block claims a slot in its bucket with a
+// wave-aggregated atomic add.  Within a class the blocks come out close to
+// list order (waves claim slots roughly in dispatch order), not exactly:
+// the digests do not depend on it (each is written at its block's index).
+constexpr int kClassBins = 32 << 6;  // length_class < 32 << mbits, mbits <= 6
+
+__global__ void __launch_bounds__(256)
+table_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kClassBins];
+  for (int i = threadIdx.x; i < kClassBins; i += 256) h[i] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    atomicAdd(&h[length_class(n_chunks(sizes[i]), mbits)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kClassBins; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// cursor[b] = blocks in classes above b (one workgroup, 2 bins per thread).
+__global__ void __launch_bounds__(1024) table_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t s[1024];
+  const int t = threadIdx.x;
+  // thread t owns bins kClassBins-1-2t and kClassBins-2-2t (descending order)
+  const uint32_t a = hist[kClassBins - 1 - 2 * t], b = hist[kClassBins - 2 - 2 * t];
+  s[t] = a + b;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = t >= d ? s[t - d] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  const uint32_t before = s[t] - (a + b);
+  cursor[kClassBins - 1 - 2 * t] = before;
+  cursor[kClassBins - 2 - 2 * t] = before + a;
+}
+
+__global__ void __launch_bounds__(256)
+table_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t* __restrict__ cursor,
+                     uint32_t* __restrict__ order) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool valid = i < n;
+  const uint32_t key = valid ? (uint32_t)length_class(n_chunks(sizes[i]), mbits) : 0xFFFFFFFFu;
+  uint64_t todo = __ballot(valid);
+  uint32_t pos = 0;
+  while (todo) {  // one atomic per distinct class in the wave; every lane leaves after its own
+    const int leader = __builtin_ctzll(todo);
+    const uint32_t k = (uint32_t)__shfl((int)key, leader, 64);
+    const uint64_t same = __ballot(key == k) & todo;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&cursor[k], (uint32_t)__builtin_popcountll(same));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (key == k) pos = base + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
+    todo &= ~same;
+  }
+  if (valid) order[pos] = (uint32_t)i;
 }
 
 // Wire emission of the signature table as the reference's FILE_BLOCK

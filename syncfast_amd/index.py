@@ -9,13 +9,26 @@ src/main.rs:111-124, and the sync endpoints, src/sync/fs.rs:53-58, 239-248,
 SQL INSERT per block, the file's bytes go through the C-ABI to the gfx950
 SHA-1 kernel and the rows are inserted in one batch.
 
-Chunking.  The reference cuts blocks with the third-party cdchunking 0.2.1
-ZPAQ chunker (src/index.rs:622-625), whose recurrence is not available here
-(CDC parity unpinned).  ``Index`` therefore takes a chunker:
-``FixedChunker(block_size)`` (the BASELINE configs) or ``BoundaryChunker``
-(any boundary function, e.g. the reference KAT boundaries); the per-block
-SHA-1, the rows, ``blocks_hash`` and every query are bit-identical to the
-reference for the same boundaries.
+Chunking -- an explicit choice, there is no default.  The reference cuts
+blocks with the third-party cdchunking 0.2.1 ZPAQ chunker (src/index.rs:
+622-625), whose recurrence is not available here (CDC parity
+unpinned).  ``index_file`` / ``index_path`` therefore need the chunker the
+caller chose when opening the index:
+  * ``BoundaryChunker(fn)`` -- the reference's mode: the boundary function is
+    the host chunker (in a Rust drop-in, the cdchunking crate itself), so the
+    blocks are the reference's by construction; every block's SHA-1 and the
+    ``blocks_hash`` come from the GPU.  ``stream=True`` hands ``fn`` the open
+    file (as ``chunker.stream(file)`` reads it) and the library re-reads the
+    file by windows (sf_index_file_blocks), so no file is held whole;
+  * ``FixedChunker(block_size)`` -- fixed tiling, the BASELINE configs' mode.
+    NOT the reference's default blocks: an index built this way only works
+    with peers that use the same mode and read a block as its row's
+    ``(offset, size)`` bytes (``read_block`` below), never by re-chunking
+    from the offset as the reference's ``read_block`` does
+    (src/sync/fs.rs:26-40).
+The per-block SHA-1, the rows, ``blocks_hash`` and every query are
+bit-identical to the reference for the same boundaries.  An ``Index`` opened
+without a chunker serves every query but refuses to index.
 
 Timestamps.  ``files.modified`` is a ``DateTime<Utc>`` (``timestamp.DateTimeUtc``):
 taken from the open file's metadata with nanosecond precision
@@ -135,21 +148,62 @@ def _seekable(f) -> bool:
 
 
 class FixedChunker:
-    """Blocks of `block_size` bytes (last one shorter); no empty blocks."""
+    """Blocks of `block_size` bytes (last one shorter); no empty blocks.
 
-    def __init__(self, block_size: int = 4096):
+    Not the reference's blocks (those are content-defined, src/index.rs:
+    622-625): use it only where every peer indexes the same way and reads a
+    block by its row's (offset, size) -- see ``read_block``."""
+
+    def __init__(self, block_size: int):
         if not 0 < block_size <= (32 << 20):
             raise ValueError("block_size must be in (0, 32 MiB]")
         self.block_size = block_size
 
 
 class BoundaryChunker:
-    """Blocks from a boundary function: fn(data: bytes) -> list of block
-    sizes (positive, summing to len(data)).  The signatures are still
-    computed by the GPU kernel (explicit-block-list entry point)."""
+    """Blocks from a host chunker -- the reference's mode (src/index.rs:
+    622-625).  fn(data: bytes) -> list of block sizes (positive, summing to
+    len(data)); with ``stream=True``, fn(file) reads an open binary file to
+    its end (as ``chunker.stream(file)`` does, src/index.rs:625) and returns
+    the sizes, and the file is re-read by windows on the library side
+    (sf_index_file_blocks) instead of being held whole.  The signatures are
+    computed by the GPU kernel (explicit-block-list entry points)."""
 
-    def __init__(self, fn: Callable[[bytes], Sequence[int]]):
+    def __init__(self, fn: Callable, stream: bool = False):
         self.fn = fn
+        self.stream = stream
+
+
+def _sizes_ok(sizes, n: int) -> List[int]:
+    sizes = [int(x) for x in sizes]
+    if any(x <= 0 for x in sizes) or sum(sizes) != n:
+        raise ValueError("boundary function must return positive sizes covering the data")
+    return sizes
+
+
+def _offsets(sizes) -> np.ndarray:
+    offs = np.zeros(len(sizes), np.uint64)
+    if len(sizes) > 1:
+        offs[1:] = np.cumsum(np.asarray(sizes, np.uint64), dtype=np.uint64)[:-1]
+    return offs
+
+
+def read_block(path, offset: int, size: int) -> bytes:
+    """The bytes of one block row: `size` bytes at `offset`.
+
+    The sync code's reader (src/sync/fs.rs:26-40) instead re-runs a fresh
+    ZPAQ chunker from `offset` and returns the first chunk it cuts; for rows
+    of the reference's content-defined blocks that is the same bytes (a
+    chunker's state resets at every boundary), for any other
+    tiling it is not.  A drop-in that indexes with fixed tiling must replace
+    read_block with this (INTEGRATION.md, "Fixed tiling"); it is correct for
+    both modes."""
+    with open(path, "rb") as f:
+        f.seek(offset)
+        b = f.read(size)
+    if len(b) != size:
+        raise SyncfastError("No such chunk in file")
+    return b
 
 
 Chunker = object  # FixedChunker | BoundaryChunker
@@ -164,14 +218,11 @@ def signatures_of_bytes(data, chunker) -> List[Tuple[int, int, bytes]]:
         # do (src/index.rs:622-625); every block's SHA-1 is computed on the
         # device through the host-memory C-ABI entry (sf_index_buffer_blocks)
         raw = bytes(data)
-        sizes = [int(s) for s in chunker.fn(raw)]
-        if any(s <= 0 for s in sizes) or sum(sizes) != len(raw):
-            raise ValueError("boundary function must return positive sizes covering the data")
+        import io
+        sizes = _sizes_ok(chunker.fn(io.BytesIO(raw)) if chunker.stream else chunker.fn(raw), len(raw))
         if not sizes:
             return []
-        offs = np.zeros(len(sizes), np.uint64)
-        offs[1:] = np.cumsum(sizes, dtype=np.uint64)[:-1]
-        rows, _ = host.index_buffer_blocks(raw, offs, np.asarray(sizes, np.uint32))
+        rows, _ = host.index_buffer_blocks(raw, _offsets(sizes), np.asarray(sizes, np.uint32))
         return host.rows_to_tuples(rows)
     raise TypeError("unknown chunker")
 
@@ -184,7 +235,17 @@ class Index:
     def __init__(self, db: sqlite3.Connection, chunker=None):
         self.db = db
         self.in_transaction = False
-        self.chunker = chunker if chunker is not None else FixedChunker(4096)
+        self.chunker = chunker  # None: queries only; index_file / index_path refuse
+
+    def _need_chunker(self):
+        if self.chunker is None:
+            raise SyncfastError(
+                "this Index was opened without a chunker: pass chunker=BoundaryChunker(fn) for the reference's "
+                "content-defined blocks (fn = the host chunker, e.g. cdchunking's ZPAQ 13 / 32 KiB, "
+                "src/index.rs:622-625) or chunker=FixedChunker(block_size) for fixed tiling (not the "
+                "reference's blocks: peers must index the same way and read blocks by (offset, size))")
+        if not isinstance(self.chunker, (FixedChunker, BoundaryChunker)):
+            raise TypeError("unknown chunker")
 
     # -- open / transactions (src/index.rs:51-74, 729-735)
     @classmethod
@@ -390,28 +451,41 @@ class Index:
     def index_file(self, path, name) -> None:
         """Cut a file into blocks and add them to the index.
 
-        With a FixedChunker the rows and blocks_hash come from one native
-        pipeline call; the blocks_hash it returns is SHA-1 over the digests in
-        offset order, which is the order the rows are inserted in and so the
-        order compute_blocks_hash's SELECT reads them back in
-        (src/index.rs:661-682) -- the same value without re-reading the rows."""
+        Native routes return the rows and the blocks_hash together: SHA-1 over
+        the digests in offset order, which is the order the rows are inserted
+        in and so the order compute_blocks_hash's SELECT reads them back in
+        (src/index.rs:661-682) -- the same value without re-reading the rows.
+        BoundaryChunker(stream=True) on a regular file: the chunker streams
+        the open file and the library re-reads it by windows
+        (sf_index_file_blocks); FixedChunker: sf_index_file / sf_index_fd;
+        a BoundaryChunker over bytes: the file's bytes and the list go to
+        sf_index_buffer_blocks."""
+        self._need_chunker()
+        ch = self.chunker
+        native = None  # (rows, blocks_hash) from a native route
         with open(path, "rb") as f:  # File::open first: same error on a missing file
             file_id, up_to_date = self.add_file(name, _mtime(f))
             if up_to_date:
                 return
-            if not isinstance(self.chunker, FixedChunker):
-                rows = signatures_of_bytes(f.read(), self.chunker)
-            elif _seekable(f):
-                rows_np, bh = host.index_file(path, self.chunker.block_size)
-            else:  # a FIFO: read sequentially from this open, as File::open + read do
-                rows_np, bh = host.index_fd(f.fileno(), self.chunker.block_size)
-        if isinstance(self.chunker, FixedChunker):
+            if isinstance(ch, FixedChunker):
+                if _seekable(f):
+                    native = host.index_file(path, ch.block_size)
+                else:  # a FIFO: read sequentially from this open, as File::open + read do
+                    native = host.index_fd(f.fileno(), ch.block_size)
+            elif ch.stream and _seekable(f):
+                size = os.fstat(f.fileno()).st_size
+                sizes = _sizes_ok(ch.fn(f), size)
+                native = host.index_file_blocks(path, _offsets(sizes), np.asarray(sizes, np.uint32))
+            else:
+                rows = signatures_of_bytes(f.read(), ch)
+        if native is not None:
+            rows_np, bh = native
             self._insert_rows(file_id, rows_np)
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.hex(), file_id))
             return
         if log.isEnabledFor(logging.DEBUG):
-            for o, s, d in rows:
-                log.debug("Adding block, offset=%d, size=%d, sha1=%s", o, s, d.hex())
+            for o, sz, d in rows:
+                log.debug("Adding block, offset=%d, size=%d, sha1=%s", o, sz, d.hex())
         self.add_blocks(file_id, rows)
         bh = self.compute_blocks_hash(file_id)
         self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.to_sql(), file_id))
@@ -438,6 +512,7 @@ class Index:
         host buffers filled by a pread thread pool, one H2D copy and one
         device launch per stage (blocks + every file's blocks_hash), reading
         overlapped with the device.  batch_bytes=0 indexes file by file."""
+        self._need_chunker()
         todo: List[Tuple[Path, PurePath]] = []
         self._index_path_rec(Path(path), PurePath(""), todo)
         if not todo:
@@ -447,10 +522,12 @@ class Index:
                 self.index_file(p, rel)
             return
         if isinstance(self.chunker, BoundaryChunker):
-            self._index_batched_boundaries(todo, batch_bytes)
+            if self.chunker.stream:  # file by file: chunker over the open file, the library re-reads it
+                for p, rel in todo:
+                    self.index_file(p, rel)
+            else:
+                self._index_batched_boundaries(todo, batch_bytes)
             return
-        if not isinstance(self.chunker, FixedChunker):
-            raise TypeError("unknown chunker")
         self._index_batched(todo, batch_bytes)
 
     def _index_path_rec(self, root: Path, rel: PurePath, todo) -> None:
@@ -540,9 +617,7 @@ class Index:
                 if up_to_date:
                     continue
                 raw = f.read()  # a FIFO in the tree is read from this open, to EOF
-            sizes = [int(x) for x in self.chunker.fn(raw)]
-            if any(x <= 0 for x in sizes) or sum(sizes) != len(raw):
-                raise ValueError("boundary function must return positive sizes covering the data")
+            sizes = _sizes_ok(self.chunker.fn(raw), len(raw))
             batch.append((file_id, nbytes, len(raw), sizes))
             parts.append(raw)
             nbytes += len(raw)

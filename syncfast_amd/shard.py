@@ -145,9 +145,22 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
     rank = dist.get_rank(group)  # shard index: the rank within `group`
     is_dst = dist.get_rank() == dst  # `dst` is a global rank, as the collectives take it
     where = device if device is not None else torch.device("cpu")
-    size_t = torch.tensor([os.path.getsize(path) if is_dst else 0], dtype=torch.int64, device=where)
+    # dst's stat, broadcast; a stat that fails on dst is broadcast as -1 so
+    # every rank raises after the broadcast instead of waiting in it
+    stat_err: Optional[BaseException] = None
+    size = 0
+    if is_dst:
+        try:
+            size = os.path.getsize(path)
+        except OSError as e:
+            stat_err, size = e, -1
+    size_t = torch.tensor([size], dtype=torch.int64, device=where)
     dist.broadcast(size_t, src=dst, group=group)
     size = int(size_t.item())
+    if size < 0:
+        if stat_err is not None:
+            raise stat_err
+        raise SfError(SF_EIO, f"index_file_sharded: rank {dst} could not stat {os.fsdecode(path)}")
     start, ln = shard_range(size, block_size, world, rank)
     failure: Optional[BaseException] = None
     try:

@@ -170,6 +170,12 @@ def file_blocks_device(digests, block_size: int, file_len: int, stream=None):
     return out
 
 
+def _check_sizes(torch, sizes, digests):
+    if (not isinstance(sizes, torch.Tensor) or sizes.numel() != digests.shape[0]
+            or sizes.dtype not in (torch.int32, torch.uint32) or sizes.device != digests.device):
+        raise ValueError("sizes must be one 32-bit size per digest, on the digests' device")
+
+
 def blocks_device(digests, sizes, stream=None):
     """FILE_BLOCK messages for an explicit block list (content-defined
     blocks, each with its own size), built on the device from a uint8[n, 20]
@@ -179,11 +185,10 @@ def blocks_device(digests, sizes, stream=None):
     import torch
     _require_device(digests, "digests", torch.uint8)
     n = digests.shape[0]
-    if sizes.numel() != n or sizes.dtype not in (torch.int32, torch.uint32) or sizes.device != digests.device:
-        raise ValueError("sizes must be one 32-bit size per digest, on the digests' device")
-    sizes = sizes.contiguous()
+    _check_sizes(torch, sizes, digests)
     need = ctypes.c_uint64(0)
     with _on(digests.device, stream):
+        sizes = sizes.contiguous()  # on the stream the kernels run on
         s = torch.cuda.current_stream(digests.device).cuda_stream
         rc = lib().sf_wire_blocks_device(None, sizes.data_ptr() if n else None, n, None, 0, ctypes.byref(need), s)
         if rc not in (0, -28):
@@ -199,15 +204,19 @@ def blocks_to_fd(digests, sizes, fd: int, stream=None) -> int:
     """The explicit list's FILE_BLOCK run written to a file descriptor, built
     on the device in chunks and streamed back (sf_wire_blocks_fd).  Returns
     the bytes written."""
+    from .device import _on, _require_device
     import torch
+    _require_device(digests, "digests", torch.uint8)  # an HBM table: the kernels read it on its device
     n = digests.shape[0]
-    if sizes.numel() != n or sizes.dtype not in (torch.int32, torch.uint32) or sizes.device != digests.device:
-        raise ValueError("sizes must be one 32-bit size per digest, on the digests' device")
-    sizes = sizes.contiguous()
-    s = (stream or torch.cuda.current_stream(digests.device)).cuda_stream
+    _check_sizes(torch, sizes, digests)
     out = ctypes.c_uint64(0)
-    check(lib().sf_wire_blocks_fd(digests.data_ptr() if n else None, sizes.data_ptr() if n else None, n, int(fd),
-                                  ctypes.byref(out), s), "sf_wire_blocks_fd")
+    # the library's streams and chunk buffers are the current device's
+    # (HostLease keys on hipGetDevice): enter the digests' device
+    with _on(digests.device, stream):
+        sizes = sizes.contiguous()  # on the stream the chunks are built after
+        s = torch.cuda.current_stream(digests.device).cuda_stream
+        check(lib().sf_wire_blocks_fd(digests.data_ptr() if n else None, sizes.data_ptr() if n else None, n,
+                                      int(fd), ctypes.byref(out), s), "sf_wire_blocks_fd")
     return out.value
 
 
@@ -216,11 +225,13 @@ def file_blocks_to_fd(digests, block_size: int, file_len: int, fd: int, stream=N
     (an SSH pipe or a file): built on the device in chunks, streamed back by
     DMA and written while the next chunk is built (sf_wire_file_blocks_fd).
     Returns the bytes written."""
+    from .device import _on, _require_device
     import torch
+    _require_device(digests, "digests", torch.uint8)
     n = digests.shape[0]
-    s = (stream or torch.cuda.current_stream(digests.device)).cuda_stream
     out = ctypes.c_uint64(0)
-    with torch.cuda.device(digests.device):
+    with _on(digests.device, stream):
+        s = torch.cuda.current_stream(digests.device).cuda_stream
         check(lib().sf_wire_file_blocks_fd(digests.data_ptr() if n else None, n, block_size, file_len, fd,
                                            ctypes.byref(out), s), "sf_wire_file_blocks_fd")
     return out.value

@@ -338,3 +338,148 @@ def test_walk_of_a_file_names_it_empty(tmp_path):
     assert len(todo) == 1 and todo[0][1] == ""
     from syncfast_amd.index import _name_str
     assert _name_str(todo[0][1]) == ""
+
+
+# ---- the drop-in's block semantics: rows read back by (offset, size) -------
+
+def _reference_read_block(path, offset, chunker_fn):
+    """What the reference's read_block does (src/sync/fs.rs:26-40): open,
+    seek to `offset`, run a FRESH chunker and return its first chunk (here
+    with the test's stand-in boundary function)."""
+    with open(path, "rb") as f:
+        f.seek(offset)
+        rest = f.read()
+    sizes = chunker_fn(rest)
+    if not sizes:
+        raise ValueError("No such chunk in file")
+    return rest[:sizes[0]]
+
+
+def _oracle_device_calls(monkeypatch):
+    """CPU stand-ins for the two explicit-list entry points (the GPU tests
+    run the real ones): the oracle's digests, in the SIG_DTYPE row layout."""
+    from syncfast_amd import host
+
+    def rows_of(raw, offs, sizes):
+        offs = np.asarray(offs, np.uint64)
+        sizes = np.asarray(sizes, np.uint32)
+        rows = np.zeros(offs.size, host.SIG_DTYPE)
+        rows["offset"], rows["size"] = offs, sizes
+        dig = oracle.index_blocks(np.frombuffer(raw, np.uint8), offs, sizes) if offs.size else np.zeros((0, 20), np.uint8)
+        rows["sha1"] = dig
+        return rows, oracle.blocks_hash(dig)
+
+    monkeypatch.setattr(host, "index_buffer_blocks", lambda data, offs, sizes: rows_of(bytes(data), offs, sizes))
+    monkeypatch.setattr(host, "index_file_blocks",
+                        lambda path, offs, sizes: rows_of(open(path, "rb").read(), offs, sizes))
+
+
+def _tree(root, seed):
+    (root / "sub").mkdir(parents=True)
+    files = {"a.bin": 50_000, "sub/b.bin": 12_345, "sub/empty": 0, "c": 1, "d": 7_777}
+    for i, (n, ln) in enumerate(files.items()):
+        (root / n).write_bytes(oracle.splitmix_bytes(ln, seed + i).tobytes())
+    return files
+
+
+def _stream_toy_cdc(f):
+    return _toy_cdc(f.read())
+
+
+def _check_read_back(idx, root, files, chunker_fn):
+    from syncfast_amd.index import read_block
+    for n in files:
+        fid, _, bh = idx.get_file(n)
+        data = (root / n).read_bytes()
+        rows = idx.list_file_blocks(fid)
+        # the rows tile the file in offset order, and every block's bytes,
+        # read back by (offset, size), hash to the stored digest
+        assert b"".join(read_block(root / n, o, s) for _h, o, s in rows) == data
+        for h, o, s in rows:
+            assert hashlib.sha1(read_block(root / n, o, s)).digest() == h.bytes
+            if chunker_fn is not None:  # the reference's re-chunking reader gets the same bytes
+                assert _reference_read_block(root / n, o, chunker_fn) == read_block(root / n, o, s)
+        assert idx.compute_blocks_hash(fid) == bh
+
+
+@pytest.mark.parametrize("stream", [False, True])
+def test_boundary_rows_read_back_by_offset_size(tmp_path, monkeypatch, stream):
+    """Index a tree with a BoundaryChunker (the reference's mode; the device
+    calls replaced by the oracle here, the GPU test below runs them), then
+    read every block back by its row's (offset, size) and re-hash it; the
+    reference's own reader (re-chunking from the offset, src/sync/fs.rs:
+    26-40) returns the same bytes for these rows, because a chunker's state
+    resets at every boundary."""
+    _oracle_device_calls(monkeypatch)
+    root = tmp_path / "tree"
+    files = _tree(root, 4000)
+    ch = BoundaryChunker(_stream_toy_cdc, stream=True) if stream else BoundaryChunker(_toy_cdc)
+    idx = Index.open(root / ".syncfast.idx", chunker=ch)
+    idx.index_path(root)
+    idx.commit()
+    _check_read_back(idx, root, files, _toy_cdc)
+
+
+def test_fixed_rows_need_the_offset_size_reader(tmp_path, monkeypatch):
+    """Why fixed tiling is opt-in: for FixedChunker rows the reference's
+    re-chunking reader returns other bytes than the row names (here with the
+    stand-in chunker), so a drop-in that indexes with fixed tiling must read
+    blocks by (offset, size) -- syncfast_amd.index.read_block, INTEGRATION.md
+    "Fixed tiling"."""
+    from syncfast_amd import host
+    from syncfast_amd.index import read_block
+    root = tmp_path / "t"
+    root.mkdir()
+    data = oracle.splitmix_bytes(20_000, 4100).tobytes()
+    (root / "f").write_bytes(data)
+
+    def fake_index_file(path, bs):
+        offs, sizes, dig = oracle.index_fixed(np.frombuffer(open(path, "rb").read(), np.uint8), bs)
+        rows = np.zeros(len(offs), host.SIG_DTYPE)
+        rows["offset"], rows["size"], rows["sha1"] = offs, sizes, dig
+        return rows, oracle.blocks_hash(dig)
+
+    monkeypatch.setattr(host, "index_file", fake_index_file)
+    idx = Index.open_in_memory(chunker=FixedChunker(4096))
+    idx.index_file(root / "f", "f")
+    rows = idx.list_file_blocks(idx.get_file("f")[0])
+    assert all(hashlib.sha1(read_block(root / "f", o, s)).digest() == h.bytes for h, o, s in rows)
+    assert any(_reference_read_block(root / "f", o, _toy_cdc) != read_block(root / "f", o, s) for _h, o, s in rows)
+
+
+def test_index_without_a_chunker_refuses_to_index(tmp_path):
+    """No silent default: an Index opened without a chunker answers queries
+    but index_file / index_path raise, naming the two modes."""
+    from syncfast_amd.index import SyncfastError
+    p = tmp_path / "f"
+    p.write_bytes(b"x" * 100)
+    idx = Index.open_in_memory()
+    with pytest.raises(SyncfastError, match="BoundaryChunker"):
+        idx.index_file(p, "f")
+    with pytest.raises(SyncfastError, match="FixedChunker"):
+        idx.index_path(tmp_path)
+    assert idx.list_files() == []
+
+
+def test_read_block_short_file(tmp_path):
+    from syncfast_amd.index import SyncfastError, read_block
+    p = tmp_path / "f"
+    p.write_bytes(b"abcdef")
+    assert read_block(p, 2, 3) == b"cde"
+    with pytest.raises(SyncfastError, match="No such chunk"):
+        read_block(p, 4, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", [False, True])
+def test_boundary_rows_read_back_on_the_gpu(gpu, tmp_path, stream):
+    """The same through the real device calls: sf_index_file_blocks (the
+    chunker streamed the open file, the library re-reads it by windows) and
+    sf_index_buffer_blocks (the bytes in memory)."""
+    root = tmp_path / "tree"
+    files = _tree(root, 4200)
+    ch = BoundaryChunker(_stream_toy_cdc, stream=True) if stream else BoundaryChunker(_toy_cdc)
+    idx = Index.open(root / ".syncfast.idx", chunker=ch)
+    idx.index_path(root)
+    idx.commit()
+    _check_read_back(idx, root, files, _toy_cdc)

@@ -167,6 +167,44 @@ def test_index_file_sharded_one_rank_fails_all_raise(tmp_path):
     assert got == {r: "SfError" for r in range(world)}
 
 
+def _missing_on_dst_worker(rank, world, port, path, bs, q):
+    import syncfast_amd.host as h
+    from syncfast_amd._lib import SfError
+    from syncfast_amd.shard import index_file_sharded
+    h.index_file_range = _fake_index_file_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        index_file_sharded(path, bs)
+        q.put((rank, "returned"))
+    except FileNotFoundError:
+        q.put((rank, "FileNotFoundError"))
+    except SfError:
+        q.put((rank, "SfError"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_index_file_sharded_missing_on_dst_all_raise(tmp_path):
+    """dst cannot stat the file: it broadcasts -1 instead of raising before
+    the broadcast, so no rank waits in a collective dst never joins; dst
+    raises the OSError, the others SfError."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_missing_on_dst_worker, args=(r, world, port, str(tmp_path / "gone"), 4096, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert got == {0: "FileNotFoundError", 1: "SfError", 2: "SfError"}
+
+
 def _subgroup_worker(rank, world, port, path, bs, q):
     import syncfast_amd.host as h
     from syncfast_amd.shard import index_file_sharded
