@@ -21,7 +21,9 @@ def bodies(path):
             name = None
             continue
         if name is not None:
-            cur.append(line.split(";")[0].rstrip())
+            # basic-block labels carry the function's index in the TU
+            # (.LBB<fn>_<bb>): another kernel added before it renumbers them
+            cur.append(re.sub(r"\.LBB\d+_", ".LBB_", line.split(";")[0].rstrip()))
     return out
 
 

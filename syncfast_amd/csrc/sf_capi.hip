@@ -138,49 +138,26 @@ inline uint64_t table_sort_min() {
 }
 constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
 
-#ifndef SF_TABLE_RADIX
-#define SF_TABLE_RADIX 0  // 1: stable rocprim radix sort of the classes (the round-2 form; A/B)
-#endif
 // Stream-ordered workspace holding the processing order of blocks [0, n) of
-// a list, longest length class first.  Default: class buckets (histogram,
-// scan, wave-aggregated atomic scatter: three small launches, near list
-// order within a class); SF_TABLE_RADIX=1 builds: a stable radix sort of
-// (length class, index) with rocprim (list order within a class).  Returns
-// nullptr (unsorted launch) if anything fails.
+// a list: stable radix sort of (length class, index) by class, descending,
+// with rocprim on `s` (list order within a class).  Stability matters: a
+// wave's 64 blocks are then alike in length AND close together in memory; a
+// class-bucketing by atomics (three small launches instead of the sort's
+// ~70 us) scattered each class's blocks across the buffer and the list ran
+// at half the rate (1410 vs 2609 GiB/s on one box, profiles/r03/bucket_sort_rejected/).
+// Returns nullptr (unsorted launch) if anything fails.
 uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
   *ws_out = nullptr;
   // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
   const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
-#if !SF_TABLE_RADIX
-  {
-    const size_t hb = (size_t)sf::kClassBins * 4;
-    uint8_t* ws = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&ws), 2 * hb + n * 4, s) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    uint32_t* hist = reinterpret_cast<uint32_t*>(ws);
-    uint32_t* cursor = reinterpret_cast<uint32_t*>(ws + hb);
-    uint32_t* order = reinterpret_cast<uint32_t*>(ws + 2 * hb);
-    const unsigned hgrid = (unsigned)std::min<uint64_t>(ceil_div(n, 256), 1024);
-    if (hipMemsetAsync(hist, 0, hb, s) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipFreeAsync(ws, s);
-      return nullptr;
-    }
-    hipLaunchKernelGGL(sf::table_hist_kernel, dim3(hgrid), dim3(256), 0, s, d_sizes, n, mbits, hist);
-    hipLaunchKernelGGL(sf::table_scan_kernel, dim3(1), dim3(1024), 0, s, hist, cursor);
-    hipLaunchKernelGGL(sf::table_scatter_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, mbits,
-                       cursor, order);
-    if (hipGetLastError() != hipSuccess) {
-      (void)hipFreeAsync(ws, s);
-      return nullptr;
-    }
-    *ws_out = ws;
-    return order;
-  }
-#endif
-  const unsigned kbits = 5u + mbits;  // class < 32 << mbits
+
+  // classes < 32 << mbits; with 4 mantissa bits (the default) the key is
+  // clamped to 8 bits (every block of 2^16+ compressions, i.e. >= 4 MiB,
+  // shares the top class) and one radix pass sorts it: ~25 us saved per
+  // call against the 11-bit key of 6 mantissa bits, which the DMA path does
+  // not need (class width 6.25 % vs 1.6 %, profiles/r03/).
+  const unsigned kbits = mbits <= 4 ? 8u : 5u + mbits;
+  const uint32_t kmax = (1u << kbits) - 1u;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   uint16_t *kin = nullptr, *kout = nullptr;
   uint32_t *iin = nullptr, *iout = nullptr;
@@ -200,7 +177,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   iin = reinterpret_cast<uint32_t*>(ws + 2 * kb);
   iout = reinterpret_cast<uint32_t*>(ws + 2 * kb + ib);
   hipLaunchKernelGGL(sf::table_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, kin, iin,
-                     mbits);
+                     mbits, kmax);
   if (hipGetLastError() != hipSuccess ||
       rocprim::radix_sort_pairs_desc(ws + 2 * kb + 2 * ib, tmp, kin, kout, iin, iout, (unsigned)n, 0u, kbits, s) !=
           hipSuccess) {

@@ -824,37 +824,40 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
 
 // ------------------------------------------- explicit lists at any offset
 // The reference's default blocks are content-defined (cdchunking ZPAQ,
-// src/index.rs:622-625): they start at any byte.  A wave of such blocks
-// still stages them through LDS by DMA (round 3):
-//   * step t stages kListPieces = 9 pieces of 16 B of every block,
-//     [a + 128t, a + 128t + 144) with a = off rounded down to 16 B, which
-//     holds the block's message bytes [off + 128t, off + 128t + 128) whatever
-//     off & 15 is (the 9th piece is the next step's first: an L2 hit);
-//   * a block's 9 pieces sit back to back in LDS (144-B slots), so one DMA
-//     wave-instruction reads ~7 blocks x 144 contiguous bytes;
-//   * each lane reads its 33 dwords from its own slot starting at dword
-//     (off & 15) >> 2 (LDS reads take per-lane addresses), and one v_perm per
-//     word shifts by off & 3 and byte-swaps at once (selector in a VGPR) --
-//     as many VALU as the aligned path's plain byte swap;
+// src/index.rs:622-625): they start at any byte.  A wave of such blocks still
+// stages them through LDS by DMA (round 3):
+//   * step t stages 9 pieces of 16 B of every block, [a + 128t, a + 128t +
+//     144) with a = off rounded down to 4 B (the DMA takes any dword-aligned
+//     source), which holds the block's message bytes [off + 128t, off + 128t
+//     + 128) whatever off & 3 is;
+//   * a block's 9 pieces sit back to back in LDS (144-B slots, 9 KiB per
+//     wave), so one DMA wave-instruction reads ~7 blocks x 144 contiguous
+//     bytes, and with a slot stride of 9 quads the lanes' ds_read_b128 are
+//     conflict-free;
+//   * one v_perm per word shifts by off & 3 and byte-swaps at once (selector
+//     in a VGPR): as many VALU as the aligned path's plain byte swap;
 //   * a lane's last chunks (the partial one with the 0x80 byte, and the
-//     length) are built from the same LDS words, so no lane ever issues its
-//     own global load; chunks past a lane's message are skipped (exec mask),
+//     length) are built from the same LDS words, so no lane issues a global
+//     load of its own; chunks past a lane's message are skipped (exec mask),
 //     which in a length-sorted wave costs ~1 chunk of 130.
+// Each 128-B line of a block is touched by two consecutive steps (the window
+// is 144 B and advances 128 B); the second touch is an L2 hit ~80 % of the
+// time with the default cache policy (PMC: 1.21x the algorithmic bytes).
+// With nt on every piece it was 1.95x; nt on the first 8 pieces and the
+// default on the 9th (a 9th DMA instruction) 1.42x, since the 8-piece window
+// itself ends in the next line (profiles/r03/).
 constexpr int kListPieces = 9;
-constexpr int kListSlotDw = kListPieces * 4;  // dwords per block slot
 
-// Cache policy of the slot DMA: the default (0), not the aligned path's nt.
-// A step's 9th piece and the next step's 1st lie in the same 128-B line; with
-// nt the L2 did not keep that line between the two steps and HBM delivered
-// it twice (FETCH_SIZE 1.95x the algorithmic bytes, profiles/r03/).
+// Cache policy of the slot DMA: the default (0), not the aligned path's nt
+// (see above).
 #ifndef SF_LIST_LOAD_AUX
 #define SF_LIST_LOAD_AUX 0
 #endif
 template <int NP>
-__device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t span16, uint32_t step,
+__device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t span4, uint32_t step,
                                              const uint32_t (&voff)[NP], uint4* wave_tile) {
   const uint64_t toff = (uint64_t)step * 128u;
-  const uint64_t left = span16 > toff ? span16 - toff : 0;
+  const uint64_t left = span4 > toff ? span4 - toff : 0;
   const uint32_t nrec = __builtin_amdgcn_readfirstlane(left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left);
   const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
   __amdgpu_buffer_rsrc_t rsrc =
@@ -886,14 +889,10 @@ __device__ __forceinline__ void finish_chunk(uint32_t (&w)[16], uint32_t size, u
   }
 }
 
-#ifndef SF_LIST_DW_READS
-#define SF_LIST_DW_READS 0  // 1: 16-B aligned pieces + per-lane dword reads at (off & 15) >> 2 (A/B)
-#endif
-// A lane's 33 message dwords of one step out of its LDS slot.
-__device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint32_t* my) {
-#pragma unroll
-  for (int m = 0; m < 33; ++m) d[m] = my[m];
-}
+// A lane's 36 dwords of one step out of its 144-B LDS slot (9 b128 reads;
+// a slot stride of 9 quads puts any 16 lanes' reads on 16 distinct bank
+// quads).  Per-lane dword reads at (off & 15) >> 2 from 16-B aligned pieces
+// were tried first: 4-way bank conflicts, no faster (profiles/r03/).
 __device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint4* myq) {
 #pragma unroll
   for (int k = 0; k < kListPieces; ++k) {
@@ -908,9 +907,9 @@ __device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint4* myq) {
 // Hash this lane's block (off, size) of an explicit list through 144-B LDS
 // slots; all 64 lanes enter together.  base = the wave's lowest block start
 // rounded down to 16 B; span = bytes from base to the wave's highest block
-// end (< 4 GiB); data 16-B aligned.  Reads only inside [base, base + span
-// rounded up to 16 B): past the span the DMA returns zeros; the up-to-15
-// bytes the rounding adds share a 16-B granule with the block's last byte.
+// end (< 4 GiB); data 16-B aligned.  The DMA is range-checked per dword
+// against span rounded up to 4 B: it reads only dwords that hold a byte of
+// the wave's span (past it, zeros).
 __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
                                                bool valid, uint64_t base, uint64_t span, uint4* __restrict__ wave_tile,
                                                Sha1& st) {
@@ -919,11 +918,7 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
   const uint32_t nch = n_chunks(size);                 // compressions of this lane's message
   const uint32_t mine = valid ? size / 64u : 0u;       // its whole data chunks
   const uint32_t nsteps = wave_max_u32(valid ? (nch + 1u) / 2u : 0u);
-#if SF_LIST_DW_READS
-  const uint32_t rel = valid ? (uint32_t)((off & ~15ull) - base) : 0u;
-#else
   const uint32_t rel = valid ? (uint32_t)((off & ~3ull) - base) : 0u;  // pieces start at the block's dword
-#endif
   uint32_t voff[kListPieces];
 #pragma unroll
   for (int j = 0; j < kListPieces; ++j) {
@@ -931,36 +926,22 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
     const uint32_t rel_b = (uint32_t)__shfl((int)rel, p / kListPieces, 64);
     voff[j] = rel_b + 16u * (uint32_t)(p % kListPieces);
   }
-#if SF_LIST_DW_READS
-  const uint32_t* my = reinterpret_cast<const uint32_t*>(wave_tile) + lane * kListSlotDw +
-                       ((uint32_t)(off >> 2) & 3u);
-#else
-  const uint4* myq = wave_tile + lane * kListPieces;  // 144-B slots: 9 quads, so 16 lanes' b128 reads hit 16 bank quads
-#endif
+  const uint4* myq = wave_tile + lane * kListPieces;  // 144-B slots
   const uint32_t sel = 0x00010203u + ((uint32_t)off & 3u) * 0x01010101u;  // shift by off & 3, then byte swap
   const uint8_t* span_ptr = data + base;
-#if SF_LIST_DW_READS
-#define LIST_SRC my
-#else
-#define LIST_SRC myq
-#endif
-#if SF_LIST_DW_READS
-  const uint64_t span16 = (span + 15u) & ~15ull;
-#else
-  const uint64_t span16 = (span + 3u) & ~3ull;  // range-checked per dword: a dword holding a block byte is read
-#endif
+  const uint64_t span4 = (span + 3u) & ~3ull;  // range-checked per dword: a dword holding a block byte is read
   // Steps in which every lane has two whole data chunks run branch-free (one
   // basic block per step: the scheduler interleaves the two compressions, as
   // in the aligned path); only the wave's last steps test each lane.
   const uint32_t nfast = wave_min_u32(valid ? mine / 2u : 0xFFFFFFFFu);
-  if (nsteps > 0) issue_pieces(span_ptr, span16, 0, voff, wave_tile);
+  if (nsteps > 0) issue_pieces(span_ptr, span4, 0, voff, wave_tile);
   uint32_t t = 0;
   for (; t < nfast; ++t) {
     uint32_t d[36];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    list_read(d, LIST_SRC);
+    list_read(d, myq);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + 1 < nsteps) issue_pieces(span_ptr, span16, t + 1, voff, wave_tile);
+    if (t + 1 < nsteps) issue_pieces(span_ptr, span4, t + 1, voff, wave_tile);
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
       uint32_t w[16];
@@ -972,9 +953,9 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
   for (; t < nsteps; ++t) {
     uint32_t d[36];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    list_read(d, LIST_SRC);
+    list_read(d, myq);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + 1 < nsteps) issue_pieces(span_ptr, span16, t + 1, voff, wave_tile);
+    if (t + 1 < nsteps) issue_pieces(span_ptr, span4, t + 1, voff, wave_tile);
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
       const uint32_t c = 2 * t + ch;
@@ -987,7 +968,6 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
       }
     }
   }
-#undef LIST_SRC
 }
 
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
@@ -1080,74 +1060,16 @@ __device__ __forceinline__ uint16_t length_class(uint32_t nch, uint32_t mbits) {
   return (uint16_t)((e << mbits) + ((nch >> (e - mbits)) & ((1u << mbits) - 1u)));  // < 32 << mbits
 }
 
+// kmax: the largest key the sort looks at (blocks of a larger class share
+// it): 255 with 4 mantissa bits, so one 8-bit radix pass sorts the list.
 __global__ void __launch_bounds__(256)
 table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __restrict__ keys,
-                  uint32_t* __restrict__ idx, uint32_t mbits) {
+                  uint32_t* __restrict__ idx, uint32_t mbits, uint32_t kmax) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  keys[i] = length_class(n_chunks(sizes[i]), mbits);
+  const uint32_t k = length_class(n_chunks(sizes[i]), mbits);
+  keys[i] = (uint16_t)(k < kmax ? k : kmax);
   idx[i] = (uint32_t)i;
-}
-
-// Bucketing by length class without a radix sort (the launcher's default):
-// a histogram of the classes, one workgroup turns it into bucket starts
-// (longest class first), and every block claims a slot in its bucket with a
-// wave-aggregated atomic add.  Within a class the blocks come out close to
-// list order (waves claim slots roughly in dispatch order), not exactly:
-// the digests do not depend on it (each is written at its block's index).
-constexpr int kClassBins = 32 << 6;  // length_class < 32 << mbits, mbits <= 6
-
-__global__ void __launch_bounds__(256)
-table_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[kClassBins];
-  for (int i = threadIdx.x; i < kClassBins; i += 256) h[i] = 0;
-  __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-    atomicAdd(&h[length_class(n_chunks(sizes[i]), mbits)], 1u);
-  __syncthreads();
-  for (int i = threadIdx.x; i < kClassBins; i += 256)
-    if (h[i]) atomicAdd(&hist[i], h[i]);
-}
-
-// cursor[b] = blocks in classes above b (one workgroup, 2 bins per thread).
-__global__ void __launch_bounds__(1024) table_scan_kernel(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t s[1024];
-  const int t = threadIdx.x;
-  // thread t owns bins kClassBins-1-2t and kClassBins-2-2t (descending order)
-  const uint32_t a = hist[kClassBins - 1 - 2 * t], b = hist[kClassBins - 2 - 2 * t];
-  s[t] = a + b;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t v = t >= d ? s[t - d] : 0u;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
-  }
-  const uint32_t before = s[t] - (a + b);
-  cursor[kClassBins - 1 - 2 * t] = before;
-  cursor[kClassBins - 2 - 2 * t] = before + a;
-}
-
-__global__ void __launch_bounds__(256)
-table_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t* __restrict__ cursor,
-                     uint32_t* __restrict__ order) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const bool valid = i < n;
-  const uint32_t key = valid ? (uint32_t)length_class(n_chunks(sizes[i]), mbits) : 0xFFFFFFFFu;
-  uint64_t todo = __ballot(valid);
-  uint32_t pos = 0;
-  while (todo) {  // one atomic per distinct class in the wave; every lane leaves after its own
-    const int leader = __builtin_ctzll(todo);
-    const uint32_t k = (uint32_t)__shfl((int)key, leader, 64);
-    const uint64_t same = __ballot(key == k) & todo;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&cursor[k], (uint32_t)__builtin_popcountll(same));
-    base = (uint32_t)__shfl((int)base, leader, 64);
-    if (key == k) pos = base + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
-    todo &= ~same;
-  }
-  if (valid) order[pos] = (uint32_t)i;
 }
 
 // Wire emission of the signature table as the reference's FILE_BLOCK

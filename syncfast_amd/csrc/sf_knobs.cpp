@@ -23,7 +23,7 @@ const KnobDef kKnobDefs[K_COUNT] = {
     {"SF_INPLACE_SERIAL", 0},           // K_INPLACE_SERIAL: lock whole range first, rows at the end
     {"SF_FADVISE", 1},                  // K_FADVISE: sequential / will-need hints on the pread route
     {"SF_NO_HOSTREG", 0},               // K_NO_HOSTREG: never page-lock caller memory
-    {"SF_TABLE_CLASS_BITS", 6},         // K_TABLE_CLASS_BITS: mantissa bits of the length class
+    {"SF_TABLE_CLASS_BITS", 4},         // K_TABLE_CLASS_BITS: mantissa bits of the length class (<= 4: 8-bit key)
     {"SF_TRACE", 0},                    // K_TRACE: sf_index_files phase times on stderr
     {"SF_TEST_INPLACE_FAIL_AT", -1},    // K_TEST_INPLACE_FAIL_AT: region k "fails" to page-lock
     {"SF_TEST_WIRE_CHUNK", 0},          // K_TEST_WIRE_CHUNK: messages per streamed chunk (0 = 2^18)
