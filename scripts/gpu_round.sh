@@ -32,6 +32,11 @@ if [ -n "$ASAN" ]; then
   # host-side ASan + UBSan of the C-ABI's host pipelines (make -C examples asan first)
   run asan_host 600 bash scripts/asan_host.sh || exit $?
 fi
+if [ -n "$CDC" ]; then
+  # the content-defined-like list through sha1_table_kernel: timing A/B
+  # against the 4 KiB list and the fixed kernel, kernel stats, PMC passes
+  run cdc_prof 900 bash scripts/cdc_prof.sh gpurun_out/cdc || exit $?
+fi
 if [ -n "$PROFILE" ]; then
   # --no-e2e: only the timed kernel launches, so rocprof's average is the
   # bench line's kernel_ms (the end-to-end leg launches 256 MiB stages)
