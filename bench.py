@@ -115,6 +115,9 @@ def parse():
     p.add_argument("--dist-timeout", type=float, default=300.0,
                    help="seconds before a stuck collective fails the run (init_process_group timeout)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--events", default="step", choices=("step", "region"),
+                   help="kernel time from HIP events around every step's launch (step) or once around the timed "
+                        "steps (region: no event between consecutive launches)")
     p.add_argument("--check-launch", action="store_true",
                    help="launcher check only (no GPU): every rank joins the process group (gloo), rank 0 "
                         "prints the world size it saw and exits")
@@ -419,7 +422,7 @@ def main():
         b = i % nbuf
         if pending[b] is not None:  # the gather that reads digs[b] must be done
             wait_gather(b, timed)
-        if timed:
+        if timed and (a.events == "step" or i == 0):
             ev[i][0].record(stream)
         if weaks is not None:
             device.index_device_weak(data, bs, out=digs[b], weak_out=weaks[b], stream=stream)
@@ -432,7 +435,7 @@ def main():
         else:
             device.index_device_batch(data, files, bs, file_hashes=True, out=digs[b], hashes_out=fhash,
                                       stream=stream, status=status)
-        if timed:
+        if timed and a.events == "step":
             ev[i][1].record(stream)
         if gather:
             r = root(i, timed)
@@ -472,13 +475,18 @@ def main():
         fin = bstream.finish()
         if fin:
             last_hashes[0] = fin[-1]
+    if a.events == "region":  # one interval over every timed launch (and the batch stream's finish)
+        ev[0][1].record(stream)
     drain(True)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
+    if a.events == "step":
+        kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
+    else:
+        kern_ms = ev[0][0].elapsed_time(ev[0][1]) / a.steps
     kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
     if distributed:
         if a.dist_backend == "gloo":

@@ -65,16 +65,25 @@ def main():
         for i in range(K):
             fns[0][1](data.data_ptr(), nf * flen, bs, d[i % 3].data_ptr(), n, ctypes.byref(nb), s.cuda_stream)
 
+    def blocks_only():  # the chained kernel with no chain jobs: its block part alone
+        arr = (ChainJob * 1)()
+        for i in range(K):
+            check(fns[0][0](data.data_ptr(), nf, flen, bs, d[i % 3].data_ptr(), arr, 0, s.cuda_stream), "chained")
+
     for _ in range(30):
         plain()
     ref = None
-    times = {name: [] for name in ["plain"] + libs}
+    names = ["plain", "blocks_only"] + libs
+    times = {name: [] for name in names}
     for _ in range(int(os.environ.get("ROUNDS", "6"))):
-        for name in ["plain"] + libs:
+        for name in names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             if name == "plain":
                 plain()
+                hs = None
+            elif name == "blocks_only":
+                blocks_only()
                 hs = None
             else:
                 hs = run_stream(fns[libs.index(name)][0])
@@ -86,7 +95,7 @@ def main():
                 if ref is None:
                     ref = got
                 assert torch.equal(got, ref), f"{name}: blocks_hash differs"
-    for name in ["plain"] + libs:
+    for name in names:
         print(f"{name}: median {statistics.median(times[name]):.4f} ms/batch  min {min(times[name]):.4f}", flush=True)
 
 

@@ -603,8 +603,11 @@ struct ChainJob {
 #ifndef SF_CHAIN_DEPTH
 #define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
 #endif
+#ifndef SF_CHAIN_PRIO
+#define SF_CHAIN_PRIO 3  // wave priority of the stream's chain waves (A/B: make variant EXTRA=-DSF_CHAIN_PRIO=0)
+#endif
 __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave) {
-  __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
+  __builtin_amdgcn_s_setprio(SF_CHAIN_PRIO);  // latency-bound chains issue first on a shared SIMD
   const uint32_t f = wave * 64 + (threadIdx.x & 63);
   if (f >= j.files) return;
   const uint8_t* p = j.runs + (uint64_t)f * j.run_len;
