@@ -428,6 +428,12 @@ def main():
             device.index_device_weak(data, bs, out=digs[b], weak_out=weaks[b], stream=stream)
         elif files is None:
             device.index_device(data, bs, out=digs[b], stream=stream)
+        elif bstream is not None and timed and i == a.steps - 1:
+            # the last batch: two column halves, then its chains' second half
+            # (inside the timed region)
+            fin = bstream.push_last(data, digs[b])
+            if fin:
+                last_hashes[0] = fin[-1]
         elif bstream is not None:
             h = bstream.push(data, digs[b])
             if h is not None:
@@ -545,11 +551,11 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     # PMC traffic of the same kernel (same machine code of the headline
     # kernel; else null: numbers from other code are stale).
-    from syncfast_amd._lib import code_object_sha256, kernel_code_sha256
+    from syncfast_amd._lib import CHAINED_KERNEL, FIXED_KERNEL, code_object_sha256, kernel_code_sha256
     traffic = None
     build = lib_sha256()
     kernels = code_object_sha256()
-    kcode = kernel_code_sha256()
+    kcode = kernel_code_sha256(symbol=CHAINED_KERNEL if bstream is not None else FIXED_KERNEL)
     try:
         with open(a.traffic_file) as f:
             tr = json.load(f)

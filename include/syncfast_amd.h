@@ -157,6 +157,18 @@ int sf_index_device_batch_chained(const void *d_data, uint32_t n_files, uint64_t
                                   uint32_t block_size, void *d_digests, const sf_chain_job *jobs,
                                   uint32_t n_jobs, void *stream);
 
+/* The same launch over block columns [col_lo, col_hi) of every file only
+ * (rows f * (file_len / block_size) + col of d_digests; the other rows are
+ * not written).  col_lo = 0, col_hi = file_len / block_size is
+ * sf_index_device_batch_chained; any other range needs 64 | blocks per file,
+ * 64 | col_lo, 64 | col_hi and col_lo < col_hi <= blocks per file, else
+ * SF_EINVAL.  A stream's LAST batch in two column halves lets the first half
+ * of its chains run inside the second launch (device.BatchStream.push_last). */
+int sf_index_device_batch_chained_cols(const void *d_data, uint32_t n_files, uint64_t file_len,
+                                       uint32_t block_size, uint64_t col_lo, uint64_t col_hi,
+                                       void *d_digests, const sf_chain_job *jobs, uint32_t n_jobs,
+                                       void *stream);
+
 /* ------------------------------------ the receiving side of a sync ---- */
 
 /* Block lookup of a sync destination.  For every FILE_BLOCK of an incoming

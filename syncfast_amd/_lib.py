@@ -31,6 +31,7 @@ EXPORTED = (
     "sf_version", "sf_strerror", "sf_device_count", "sf_set_device", "sf_release_host_cache",
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
+    "sf_index_device_batch_chained_cols",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
@@ -82,6 +83,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_index_device_fixed_weak.argtypes = [vp, u64, u32, vp, vp, u64, pu64, vp]
     L.sf_index_device_blocks_weak.argtypes = [vp, u64, vp, vp, u64, vp, vp, vp, vp]
     L.sf_index_device_batch_chained.argtypes = [vp, u32, u64, u32, vp, ctypes.POINTER(ChainJob), u32, vp]
+    L.sf_index_device_batch_chained_cols.argtypes = [vp, u32, u64, u32, u64, u64, vp, ctypes.POINTER(ChainJob), u32,
+                                                     vp]
     L.sf_index_device_batch.argtypes = [vp, u64, ctypes.POINTER(FileDesc), u32, u32, vp, u64, vp, vp, pu64, vp, vp]
     L.sf_fill_splitmix_device.argtypes = [vp, u64, u64, u64, vp]
     L.sf_wire_file_blocks_device.argtypes = [vp, u64, u32, u64, vp, u64, pu64, vp]
@@ -195,13 +198,19 @@ def _code_objects(path: str):
         pos = fat.find(magic, pos + 1)
 
 
-def kernel_code_sha256(path: str = None,
-                       symbol: str = "_ZN2sf17sha1_fixed_kernelILi128ELi1ELb0EEEvPKhmjmPhNS_11PadScheduleEPj") -> str:
+FIXED_KERNEL = "_ZN2sf17sha1_fixed_kernelILi128ELi1ELb0EEEvPKhmjmPhNS_11PadScheduleEPj"
+CHAINED_KERNEL = "_ZN2sf25sha1_fixed_chained_kernelILi128EEEvPKhmjmPhNS_11PadScheduleENS_8ChainJobES5_jjj"
+
+
+def kernel_code_sha256(path: str = None, symbol: str = FIXED_KERNEL) -> str:
     """SHA-256 of one kernel's machine code (its bytes in the gfx950 code
     object's .text, located through .symtab): what the GPU runs for that
     kernel.  Other kernels of the same translation unit can change without
     changing it.  bench.py keys the PMC traffic of profiles/traffic.json on it
-    for the headline kernel (sha1_fixed_kernel<128, 1, false>)."""
+    for the headline kernel (sha1_fixed_kernel<128, 1, false>); config 3's
+    line names sha1_fixed_chained_kernel<128>'s (CHAINED_KERNEL), whose
+    block rate depends on how its block part was compiled (DESIGN.md
+    section 3.3b)."""
     import hashlib
     import struct
     for _, co in _code_objects(path):

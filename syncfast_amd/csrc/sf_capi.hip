@@ -494,11 +494,24 @@ static int sf_index_device_batch_body(const void* d_data, uint64_t len, const sf
 
 int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t file_len, uint32_t block_size,
                                   void* d_digests, const sf_chain_job* jobs, uint32_t n_jobs, void* stream) {
+  const uint64_t nbf = block_size ? file_len / block_size : 0;
+  return sf_index_device_batch_chained_cols(d_data, n_files, file_len, block_size, 0, nbf, d_digests, jobs, n_jobs,
+                                            stream);
+}
+
+int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uint64_t file_len, uint32_t block_size,
+                                       uint64_t col_lo, uint64_t col_hi, void* d_digests, const sf_chain_job* jobs,
+                                       uint32_t n_jobs, void* stream) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
   if (n_files && (file_len == 0 || file_len % block_size)) return SF_EINVAL;
   if (n_jobs > 2 || (n_jobs && !jobs)) return SF_EINVAL;
-  const uint64_t total = n_files ? (file_len / block_size) * n_files : 0;
+  const uint64_t nbf = file_len / block_size;
+  // the whole files, or a column range in whole block waves of whole-wave files
+  const bool whole = col_lo == 0 && col_hi == nbf;
+  if (n_files && !whole && (col_lo >= col_hi || col_hi > nbf || nbf % 64 || col_lo % 64 || col_hi % 64))
+    return SF_EINVAL;
+  const uint64_t total = n_files ? nbf * n_files : 0;
   if (total && (!d_data || !d_digests)) return SF_EINVAL;
   if (total > launch_max_blocks()) return SF_EINVAL;  // one launch per batch: split the batch
   sf::ChainJob cj[2] = {};
@@ -523,7 +536,8 @@ int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t
   // grid: C mixed workgroups (1 chain wave + 3 block waves), then 4 block
   // waves per workgroup for the rest
   const uint64_t C_ = cj[0].waves + cj[1].waves;
-  const uint64_t bwaves = ceil_div(total, 64);
+  const uint32_t wpf = whole ? 1u : (uint32_t)(nbf / 64), wpp = whole ? 1u : (uint32_t)((col_hi - col_lo) / 64);
+  const uint64_t bwaves = whole ? ceil_div(total, 64) : (uint64_t)n_files * wpp;
 #if defined(SF_TUNING) && defined(SF_CHAIN_SOLO)
   const uint64_t rest = bwaves;  // A/B only: chain workgroups hold the chain wave alone
 #else
@@ -533,7 +547,8 @@ int sf_index_device_batch_chained(const void* d_data, uint32_t n_files, uint64_t
   if (grid == 0) return SF_OK;
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),
                      static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
-                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1]);
+                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1], wpf, wpp,
+                     whole ? 0u : (uint32_t)(col_lo / 64));
   return hip_err(hipGetLastError());
 }
 

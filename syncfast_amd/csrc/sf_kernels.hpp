@@ -557,6 +557,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 // file of a batch has the same run length); q must be 16-B aligned.
 template <int D>
 __device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restrict__ q, uint32_t nch) {
+  static_assert(D % 2 == 0, "chunks are refilled in pairs");
   if (nch == 0) return;
   uint4 buf[D][4];
 #pragma unroll
@@ -578,9 +579,15 @@ __device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restri
           w[4 * i + 2] = bswap32(buf[k][i].z);
           w[4 * i + 3] = bswap32(buf[k][i].w);
         }
-        const uint32_t nx = c + D < nch ? c + D : nch - 1;
+        // refill two chunks (one 128-B line) back to back after every
+        // second chunk, so each line of the run is fetched into L1 once
+        if (k & 1) {
+          const uint32_t n0 = c - 1 + D < nch ? c - 1 + D : nch - 1, n1 = c + D < nch ? c + D : nch - 1;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)nx * 4 + i];
+          for (int i = 0; i < 4; ++i) buf[k - 1][i] = q[(uint64_t)n0 * 4 + i];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)n1 * 4 + i];
+        }
         st.compress(w);
       }
     }
@@ -644,7 +651,7 @@ template <int TILE>
 __global__ void __launch_bounds__(kThreads, 1)
 sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
                           uint8_t* __restrict__ digests, const PadSchedule pad, const ChainJob j0,
-                          const ChainJob j1) {
+                          const ChainJob j1, const uint32_t wpf, const uint32_t wpp, const uint32_t poff) {
   // Chain waves are spread one per workgroup: workgroup g < C runs chain
   // wave g as its wave 0 (job 0's waves first) and block waves 3g..3g+2 as
   // its waves 1-3; the other workgroups run 4 block waves each.  So no CU
@@ -672,6 +679,9 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
     bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
   }
 #endif
+  // A column-range launch (wpp < wpf: every file's block waves [poff,
+  // poff + wpp) of its wpf) maps its wave bw to the file's wave.
+  if (wpp != wpf) bw = (uint64_t)((uint32_t)bw / wpp) * wpf + poff + (uint32_t)bw % wpp;
   fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, bw, smem + wid * 64 * (TILE / 16));
 }
 

@@ -240,8 +240,13 @@ class BatchStream:
     first half of batch i-1's, so a chain needs only half the latency cover.
     push() returns the blocks_hash tensor (uint8[n_files, 20]) of the batch
     whose chains this launch completes (i-2 split, i-1 unsplit), or None;
-    finish() returns the remaining ones in batch order.  A batch's digest
-    table must stay alive until its hashes have been returned."""
+    finish() returns the remaining ones in batch order.  push_last(data,
+    digests) pushes the stream's last batch and finishes: it returns every
+    remaining blocks_hash tensor, and with split chains it hashes that batch
+    in two column halves, so the first half of its chains runs beside the
+    second half's blocks and only the second half of its chains runs alone.
+    A batch's digest table must stay alive until its hashes have been
+    returned."""
 
     def __init__(self, n_files: int, file_len: int, block_size: int, stream: Optional[torch.cuda.Stream] = None,
                  split: bool = True):
@@ -261,15 +266,16 @@ class BatchStream:
         return ChainJob(d.data_ptr(), self.n_files, part, self.nbf, state.data_ptr() if state is not None else None,
                         h.data_ptr() if part != 1 else None)
 
-    def _launch(self, data, digests, jobs, ref):
+    def _launch(self, data, digests, jobs, ref, cols=None):
         from ._lib import ChainJob
         arr = (ChainJob * max(len(jobs), 1))(*jobs)
+        lo, hi = cols if cols is not None else (0, self.nbf)
         with _on(ref.device, self.stream):
-            check(lib().sf_index_device_batch_chained(
+            check(lib().sf_index_device_batch_chained_cols(
                 data.data_ptr() if data is not None else None, self.n_files if data is not None else 0,
-                self.file_len, self.block_size, digests.data_ptr() if digests is not None else None,
+                self.file_len, self.block_size, lo, hi, digests.data_ptr() if digests is not None else None,
                 arr, len(jobs), _stream_ptr(ref, self.stream)),
-                "sf_index_device_batch_chained")
+                "sf_index_device_batch_chained_cols")
 
     def _step_jobs(self):
         """Chain jobs for the next launch; advances the pipeline state."""
@@ -294,11 +300,14 @@ class BatchStream:
             self._b = None
         return jobs, done
 
-    def push(self, data: torch.Tensor, digests: torch.Tensor):
+    def _check_batch(self, data, digests):
         _require_device(data, "data", torch.uint8)
         _require_device(digests, "digests", torch.uint8, data.device)
         if data.numel() != self.n_files * self.file_len or digests.numel() < 20 * self.n_files * self.nbf:
             raise ValueError("batch or digest table has the wrong size")
+
+    def push(self, data: torch.Tensor, digests: torch.Tensor):
+        self._check_batch(data, digests)
         # the chain states and this batch's blocks_hash table are allocated on
         # the stream the launches run on, like every other output here
         with _on(data.device, self.stream):
@@ -306,6 +315,40 @@ class BatchStream:
             self._launch(data, digests, jobs, data)
             self._b = (digests, torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device))
         return done
+
+    def _half_cols(self):
+        """Column split of a last batch: the first half of every chain (part
+        1: bytes [0, 64 * half) of the run) reads digests [0, cut) only."""
+        if not self.split or self.nbf % 64 or self.nbf < 128:
+            return None
+        half = (self.nbf * 20 // 64) // 2  # data chunks of part 1 (as the launcher computes them)
+        need = (half * 64 + 19) // 20  # digests part 1 reads
+        cut = (need + 63) // 64 * 64  # in whole block waves
+        return cut if cut < self.nbf else None
+
+    def push_last(self, data: torch.Tensor, digests: torch.Tensor):
+        """Push the stream's last batch and finish; returns every remaining
+        blocks_hash tensor in batch order."""
+        self._check_batch(data, digests)
+        cut = self._half_cols()
+        if cut is None:
+            done = self.push(data, digests)
+            return ([done] if done is not None else []) + self.finish()
+        out = []
+        with _on(data.device, self.stream):
+            # columns [0, cut) beside the jobs push() would run ...
+            jobs, done = self._step_jobs()
+            self._launch(data, digests, jobs, data, (0, cut))
+            if done is not None:
+                out.append(done)
+            # ... then columns [cut, end) beside the next jobs, which include
+            # the first half of this batch's chains (its digests [0, cut) exist)
+            self._b = (digests, torch.empty((self.n_files, 20), dtype=torch.uint8, device=data.device))
+            jobs, done = self._step_jobs()
+            self._launch(data, digests, jobs, data, (cut, self.nbf))
+            if done is not None:
+                out.append(done)
+        return out + self.finish()
 
     def finish(self):
         out = []

@@ -116,7 +116,7 @@ def test_config5_32gib_64k_properties(gpu):
     assert host.blocks_hash(torch.cat([h1, h2]).cpu().numpy()) == host.blocks_hash(dig)
 
 
-@pytest.mark.parametrize("mode", ["stream", "staged"])
+@pytest.mark.parametrize("mode", ["stream", "stream_last", "staged"])
 def test_config3_1024x8mib_every_digest_and_blocks_hash(gpu, mode):
     # configs[2] at full size: 1024 files x 8 MiB, every digest and every
     # file's blocks_hash vs the multi-threaded C oracle
@@ -127,6 +127,11 @@ def test_config3_1024x8mib_every_digest_and_blocks_hash(gpu, mode):
         dig = torch.empty((nf * flen // bs, 20), dtype=torch.uint8, device=gpu)
         assert st.push(data, dig) is None
         (fh,) = st.finish()
+    elif mode == "stream_last":  # bench.py's last step: two column halves (cut at block 1024 of 2048)
+        st = device.BatchStream(nf, flen, bs)
+        assert st._half_cols() == 1024
+        dig = torch.empty((nf * flen // bs, 20), dtype=torch.uint8, device=gpu)
+        (fh,) = st.push_last(data, dig)
     else:
         dig, _, fh = device.index_device_batch(data, [(i * flen, flen) for i in range(nf)], bs)
     dig, fh = dig.cpu().numpy(), fh.cpu().numpy()
