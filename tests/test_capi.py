@@ -341,3 +341,15 @@ def test_pmc_traffic_averages_full_shard_launches(tmp_path):
             w.writerow({"Dispatch_Id": i, "Grid_Size": grid, "Kernel_Name": name, "Counter_Name": "FETCH_SIZE",
                         "Counter_Value": v})
     assert mod.avg(str(p), "FETCH_SIZE") == (101.0, 2)
+
+
+def test_chained_kernel_is_the_measured_one():
+    # sha1_fixed_chained_kernel<128>'s block part ran at the plain kernel's
+    # rate only in some compiled forms: the committed
+    # launch-sequence measurement names the machine code it measured
+    import json
+    from syncfast_amd._lib import CHAINED_KERNEL, kernel_code_sha256
+    with open(os.path.join(ROOT, "profiles", "r03", "c3", "chained_kernel.json")) as f:
+        rec = json.load(f)
+    assert kernel_code_sha256(symbol=CHAINED_KERNEL) == rec["kernel_code_sha256"], \
+        "the chained kernel changed: re-measure with scripts/c3_seq.sh and update the record"
