@@ -545,6 +545,11 @@ int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uin
 #endif
   const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
   if (grid == 0) return SF_OK;
+#ifndef SF_NO_CHAIN_HELPER
+  if (total == 0) {  // chains alone (a stream's finish): each chain wave gets a schedule-building helper wave
+    return launch_chain_helper(cj[0], cj[1], as_stream(stream));
+  }
+#endif
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),
                      static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
                      static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1], wpf, wpp,

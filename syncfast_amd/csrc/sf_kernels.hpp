@@ -25,7 +25,7 @@
 #include <stdint.h>
 
 #include "../../include/syncfast_amd.h"
-#include "sha1_device.hpp"
+#include "sf_chain.hpp"
 
 namespace sf {
 
@@ -71,12 +71,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return uniform_u64(v);
 }
 
-__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
-  uint32_t v;
-  __builtin_memcpy(&v, p, 4);
-  return v;
-}
-
 // 64 bytes at any byte address (four 16-B loads; unaligned global access).
 __device__ __forceinline__ void ld_chunk_any(uint4 (&v)[4], const uint8_t* p) {
 #pragma unroll
@@ -87,37 +81,6 @@ __device__ __forceinline__ void ld_chunk_any(uint4 (&v)[4], const uint8_t* p) {
 __device__ __forceinline__ void ld_chunk_al(uint4 (&v)[4], const uint32_t* p) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) __builtin_memcpy(&v[k], p + 4 * k, 16);
-}
-
-// Number of SHA-1 compressions for a message of `size` bytes.
-__device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
-
-// Chunk c (0-based) of the padded message of a block of `size` bytes that
-// starts at p (global memory).  Reads only bytes [0, size) of the block.
-__device__ __forceinline__ void build_tail_chunk(uint32_t (&w)[16], const uint8_t* p, uint32_t size,
-                                                 uint32_t c, uint32_t nch) {
-  const int64_t rem = (int64_t)size - (int64_t)c * 64;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int64_t v = rem - 4 * j;  // valid data bytes in word j
-    uint32_t x = 0;
-    const uint8_t* q = p + (uint64_t)c * 64 + 4 * j;
-    if (v >= 4) {
-      x = bswap32(ld_u32_any(q));
-    } else if (v > 0) {
-      uint32_t y = (uint32_t)q[0] << 24;
-      if (v > 1) y |= (uint32_t)q[1] << 16;
-      if (v > 2) y |= (uint32_t)q[2] << 8;
-      x = y | (0x80u << (8 * (3 - (int)v)));
-    } else if (v == 0) {
-      x = 0x80000000u;
-    }
-    w[j] = x;
-  }
-  if (c == nch - 1) {
-    w[14] = size >> 29;
-    w[15] = size << 3;
-  }
 }
 
 // K_t + W_t of the padding-only chunk ending a block of `bytes` bytes
@@ -594,22 +557,6 @@ __device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restri
   }
 }
 
-// One per-file blocks_hash chain job (src/index.rs:661-682) of a batch of
-// equal-size files: one lane per file over its run of run_len digest bytes,
-// data chunks [lo, hi) (64-B units) of the run.  part 0 = the whole chain;
-// part 1 = chunks [0, hi), the 5-word SHA-1 state saved to state[f]; part 2
-// = resume from state[f], chunks [lo, end) + the padding chunk(s), hash to
-// hashes[f].
-struct ChainJob {
-  const uint8_t* runs;
-  uint8_t* state;
-  uint8_t* hashes;
-  uint32_t files, run_len, lo, hi, part, waves;  // waves = chain waves (64 files each)
-};
-
-#ifndef SF_CHAIN_DEPTH
-#define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
-#endif
 #ifndef SF_CHAIN_PRIO
 #define SF_CHAIN_PRIO 3  // wave priority of the stream's chain waves (A/B: make variant EXTRA=-DSF_CHAIN_PRIO=0)
 #endif

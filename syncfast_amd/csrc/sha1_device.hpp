@@ -170,4 +170,42 @@ struct Adler {
   }
 };
 
+// ------------------------------------------------ message helpers
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+
+// Number of SHA-1 compressions for a message of `size` bytes.
+__device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
+
+// Chunk c (0-based) of the padded message of a block of `size` bytes that
+// starts at p (global memory).  Reads only bytes [0, size) of the block.
+__device__ __forceinline__ void build_tail_chunk(uint32_t (&w)[16], const uint8_t* p, uint32_t size,
+                                                 uint32_t c, uint32_t nch) {
+  const int64_t rem = (int64_t)size - (int64_t)c * 64;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int64_t v = rem - 4 * j;  // valid data bytes in word j
+    uint32_t x = 0;
+    const uint8_t* q = p + (uint64_t)c * 64 + 4 * j;
+    if (v >= 4) {
+      x = bswap32(ld_u32_any(q));
+    } else if (v > 0) {
+      uint32_t y = (uint32_t)q[0] << 24;
+      if (v > 1) y |= (uint32_t)q[1] << 16;
+      if (v > 2) y |= (uint32_t)q[2] << 8;
+      x = y | (0x80u << (8 * (3 - (int)v)));
+    } else if (v == 0) {
+      x = 0x80000000u;
+    }
+    w[j] = x;
+  }
+  if (c == nch - 1) {
+    w[14] = size >> 29;
+    w[15] = size << 3;
+  }
+}
+
 }  // namespace sf
