@@ -267,6 +267,19 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   if (S == 1) {
     int rc = launch_fixed(base, nbf * nfiles * (uint64_t)bs, bs, nbf * nfiles, dig, s);
     if (rc) return rc;
+    if (nbf % 4 == 0 && nbf * 20 <= 0xFFFFFFF0ull && (reinterpret_cast<uintptr_t>(dig) & 15) == 0) {
+      // 16-B aligned runs: chains with schedule-building helper waves
+      sf::ChainJob j = {}, none = {};
+      j.runs = dig;
+      j.hashes = fh;
+      j.files = nfiles;
+      j.run_len = (uint32_t)(nbf * 20);
+      j.lo = 0;
+      j.hi = j.run_len / 64;
+      j.part = 0;
+      j.waves = (uint32_t)ceil_div(nfiles, 64);
+      return launch_chain_helper(j, none, s);
+    }
     hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3((unsigned)ceil_div(nfiles, 64)), dim3(64), 0, s, dig, nbf * 20,
                        nfiles, (uint32_t)(nbf * 20), fh);
     return hip_err(hipGetLastError());
