@@ -452,14 +452,6 @@ def main():
         for b in sorted((b for b in range(nbuf) if pending[b] is not None), key=lambda b: pending[b][2]):
             wait_gather(b, timed)
 
-    # Setup (not a step): clock ramp, untimed, no gather.
-    t_ramp = time.perf_counter()
-    while time.perf_counter() - t_ramp < a.ramp_s:
-        if weaks is not None:
-            device.index_device_weak(data, bs, out=digs[0], weak_out=weaks[0], stream=stream)
-        else:
-            device.index_device(data, bs, out=digs[0], stream=stream)
-        torch.cuda.synchronize()
     for i in range(a.warmup):
         step(i, False)
     if bstream is not None:
@@ -470,6 +462,16 @@ def main():
         # every root here (untimed), so no timed step pays for a connection
         for r in range(world):
             gather_digests(digs[0], total, bs, dst=r)
+    # Setup (not a step): clock ramp, untimed, no gather -- after the warmup,
+    # so that every config's timed steps follow the same busy GPU (a batch
+    # stream's warmup ends with its light finish launches).
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < a.ramp_s:
+        if weaks is not None:
+            device.index_device_weak(data, bs, out=digs[0], weak_out=weaks[0], stream=stream)
+        else:
+            device.index_device(data, bs, out=digs[0], stream=stream)
+        torch.cuda.synchronize()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()

@@ -551,12 +551,15 @@ int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uin
   const uint64_t C_ = cj[0].waves + cj[1].waves;
   const uint32_t wpf = whole ? 1u : (uint32_t)(nbf / 64), wpp = whole ? 1u : (uint32_t)((col_hi - col_lo) / 64);
   const uint64_t bwaves = whole ? ceil_div(total, 64) : (uint64_t)n_files * wpp;
-#if defined(SF_TUNING) && defined(SF_CHAIN_SOLO)
-  const uint64_t rest = bwaves;  // A/B only: chain workgroups hold the chain wave alone
+#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
+  const unsigned grid = (unsigned)(ceil_div(C_, 4) + ceil_div(bwaves, sf::kWavesPerWG));  // A/B only
+#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
+  const uint64_t rest = bwaves > 3 * C_ * SF_CHAIN_UNITS ? bwaves - 3 * C_ * SF_CHAIN_UNITS : 0;  // A/B only
+  const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
 #else
   const uint64_t rest = bwaves > 3 * C_ ? bwaves - 3 * C_ : 0;
-#endif
   const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
+#endif
   if (grid == 0) return SF_OK;
 #ifndef SF_NO_CHAIN_HELPER
   if (total == 0) {  // chains alone (a stream's finish): each chain wave gets a schedule-building helper wave

@@ -609,18 +609,40 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
   const uint32_t C = j0.waves + j1.waves;  // chain waves
   const uint32_t g = blockIdx.x;
   uint64_t bw;
+#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
+  // A/B only: four chain waves per workgroup (ceil(C/4) chain workgroups)
+  const uint32_t CW = (C + 3) / 4;
+  if (g < CW) {
+    const uint32_t ci = g * 4 + wid;
+    if (ci < j0.waves) chain_job(j0, ci);
+    else if (ci < C) chain_job(j1, ci - j0.waves);
+    return;
+  }
+  bw = (uint64_t)(g - CW) * kWavesPerWG + wid;
+#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
+  // A/B only: the mixed workgroups' block waves hash SF_CHAIN_UNITS units each
   if (g < C) {
     if (wid == 0) {
       if (g < j0.waves) chain_job(j0, g);
       else chain_job(j1, g - j0.waves);
       return;
     }
-#if defined(SF_TUNING) && defined(SF_CHAIN_SOLO)
-    return;  // A/B only: the chain wave's workgroup hashes no blocks
-  } else {
-    bw = (uint64_t)(g - C) * kWavesPerWG + wid;
+    const uint64_t first = ((uint64_t)g * 3 + (wid - 1)) * SF_CHAIN_UNITS;
+    for (int k = 0; k < SF_CHAIN_UNITS; ++k) {
+      uint64_t u = first + k;
+      if (wpp != wpf) u = (uint64_t)((uint32_t)u / wpp) * wpf + poff + (uint32_t)u % wpp;
+      fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, u, smem + wid * 64 * (TILE / 16));
+    }
+    return;
   }
+  bw = (uint64_t)C * 3 * SF_CHAIN_UNITS + (uint64_t)(g - C) * kWavesPerWG + wid;
 #else
+  if (g < C) {
+    if (wid == 0) {
+      if (g < j0.waves) chain_job(j0, g);
+      else chain_job(j1, g - j0.waves);
+      return;
+    }
     bw = (uint64_t)g * 3 + (wid - 1);
   } else {
     bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
