@@ -115,9 +115,12 @@ def parse():
     p.add_argument("--dist-timeout", type=float, default=300.0,
                    help="seconds before a stuck collective fails the run (init_process_group timeout)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--events", default="step", choices=("step", "region"),
+    p.add_argument("--events", default="auto", choices=("auto", "step", "region"),
                    help="kernel time from HIP events around every step's launch (step) or once around the timed "
-                        "steps (region: no event between consecutive launches)")
+                        "steps (region: no event between consecutive launches).  auto = region on one rank "
+                        "(a timing event between two launches costs a batch stream's chain loads ~1.5 %%, "
+                        "profiles/r03/c3/seq), step with several ranks (the multi block splits kernel time "
+                        "from gather waits)")
     p.add_argument("--check-launch", action="store_true",
                    help="launcher check only (no GPU): every rank joins the process group (gloo), rank 0 "
                         "prints the world size it saw and exits")
@@ -322,6 +325,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.events == "auto":
+        a.events = "region" if world == 1 else "step"
     if a.check_launch:
         return check_launch(a, world, rank)
 
@@ -621,6 +626,7 @@ def main():
         "lib_sha256": build,
         "code_object_sha256": kernels,
         "kernel_code_sha256": kcode,
+        "events": a.events,
         "multi": multi,
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,

@@ -1,7 +1,8 @@
 """Config 3 launch-duration decomposition (not a test): back-to-back
 segments of K launches with no host sync in between -- plain fixed kernel,
 then per library the chained kernel with no chain jobs and a batch stream
-(K-1 pushes + push_last) -- repeated ROUNDS times, so a kernel trace (scripts/c3_seq.sh)
+(K-1 pushes + push_last) -- repeated ROUNDS times (EVENTS=1: a timing event
+recorded after every launch, as bench.py does), so a kernel trace (scripts/c3_seq.sh)
 gives every launch's duration under the same clock and power state.
 
 usage: python scripts/c3_seq.py [lib.so ...]   (default: the in-tree library)
@@ -50,17 +51,29 @@ def main():
             check(self.f(data_.data_ptr() if data_ is not None else None, nf if data_ is not None else 0, flen, bs,
                          lo, hi, digests.data_ptr() if digests is not None else None, arr, len(jobs), s.cuda_stream),
                   "chained_cols")
+            mark()
+
+    events = os.environ.get("EVENTS") == "1"  # a timing event after every launch, as bench.py's step mode
+    evs = []
+
+    def mark():
+        if events:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            evs.append(e)
 
     nb = ctypes.c_uint64()
     keep = []
     for r in range(rounds + 1):  # round 0 warms up
         for i in range(K):
             fns[0][1](data.data_ptr(), nf * flen, bs, d[i % 3].data_ptr(), n, ctypes.byref(nb), s.cuda_stream)
+            mark()
         arr = (ChainJob * 1)()
         for f, _ in fns:
             for i in range(K):
                 check(f(data.data_ptr(), nf, flen, bs, 0, n // nf, d[i % 3].data_ptr(), arr, 0, s.cuda_stream),
                       "blocks_only")
+                mark()
             st = Stream(f)
             for i in range(K - 1):
                 h = st.push(data, d[i % 3])

@@ -2,7 +2,7 @@
 # Kernel trace of scripts/c3_seq.py (config 3 launch durations, back to back).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/c3s
+OUT=${OUT:-gpurun_out/c3s}
 mkdir -p $OUT
 echo "== seq"
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$OUT/seq" -o run -- python3 scripts/c3_seq.py "$@" > "$OUT/seq.log" 2>&1
