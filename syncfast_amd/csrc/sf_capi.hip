@@ -546,31 +546,14 @@ int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uin
     cj[k].part = j.part;
     cj[k].waves = (uint32_t)ceil_div(j.n_files, 64);  // chain waves, one per workgroup
   }
-  // grid: C mixed workgroups (1 chain wave + 3 block waves), then 4 block
-  // waves per workgroup for the rest
-  const uint64_t C_ = cj[0].waves + cj[1].waves;
   const uint32_t wpf = whole ? 1u : (uint32_t)(nbf / 64), wpp = whole ? 1u : (uint32_t)((col_hi - col_lo) / 64);
   const uint64_t bwaves = whole ? ceil_div(total, 64) : (uint64_t)n_files * wpp;
-#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
-  const unsigned grid = (unsigned)(ceil_div(C_, 4) + ceil_div(bwaves, sf::kWavesPerWG));  // A/B only
-#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
-  const uint64_t rest = bwaves > 3 * C_ * SF_CHAIN_UNITS ? bwaves - 3 * C_ * SF_CHAIN_UNITS : 0;  // A/B only
-  const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
-#else
-  const uint64_t rest = bwaves > 3 * C_ ? bwaves - 3 * C_ : 0;
-  const unsigned grid = (unsigned)(C_ + ceil_div(rest, sf::kWavesPerWG));
-#endif
-  if (grid == 0) return SF_OK;
 #ifndef SF_NO_CHAIN_HELPER
-  if (total == 0) {  // chains alone (a stream's finish): each chain wave gets a schedule-building helper wave
-    return launch_chain_helper(cj[0], cj[1], as_stream(stream));
-  }
+  if (total == 0) return launch_chain_helper(cj[0], cj[1], as_stream(stream));  // chains alone: helper waves
 #endif
-  hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, as_stream(stream),
-                     static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
-                     static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1], wpf, wpp,
-                     whole ? 0u : (uint32_t)(col_lo / 64));
-  return hip_err(hipGetLastError());
+  return launch_chained(static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
+                        static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1], bwaves, wpf, wpp,
+                        whole ? 0u : (uint32_t)(col_lo / 64), as_stream(stream));
 }
 
 int sf_wire_file_blocks_device(const void* d_digests, uint64_t n_blocks, uint32_t block_size, uint64_t file_len,

@@ -35,3 +35,16 @@ namespace sfi {
 // j1 on `stream`; SF_OK or the launch error.
 int launch_chain_helper(const sf::ChainJob& j0, const sf::ChainJob& j1, hipStream_t stream);
 }  // namespace sfi
+
+namespace sf {
+struct PadSchedule;
+}
+
+namespace sfi {
+// sha1_fixed_chained_kernel<128> (sf_stream.hip): `bwaves` block waves of 64
+// blocks (a column range: wpp of every file's wpf waves from poff) beside
+// the chain waves of j0 and j1.
+int launch_chained(const uint8_t* data, uint64_t len, uint32_t bs, uint64_t nblocks, uint8_t* digests,
+                   const sf::PadSchedule& pad, const sf::ChainJob& j0, const sf::ChainJob& j1, uint64_t bwaves,
+                   uint32_t wpf, uint32_t wpp, uint32_t poff, hipStream_t stream);
+}  // namespace sfi

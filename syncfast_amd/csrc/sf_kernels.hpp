@@ -506,6 +506,7 @@ __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uin
   st.store(out + (uint64_t)f * 20);
 }
 
+#ifndef SF_STREAM_TU  // kernels of sf_capi.hip only (sf_stream.hip includes the device functions)
 // Stand-alone chains (no stages): one lane per file over its whole run.
 __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
@@ -513,6 +514,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
   chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr, 0);
 }
+#endif
 
 // Deep-prefetch form of sha1_stream_range for chains that run beside a
 // streaming block launch (their digest loads miss to HBM under load): D
@@ -586,75 +588,10 @@ __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave) {
   st.store(j.hashes + (uint64_t)f * 20);
 }
 
-// Equal-size many-file batches as a stream (BASELINE configs[2], batch after
-// batch): ONE launch hashes every block of batch i (fixed_wave) and, in its
-// first workgroups, up to two chain jobs of earlier batches (j0 then j1):
-// with split chains, the second half of batch i-2's and the first half of
-// batch i-1's.  Their digest tables and saved states were completed by
-// earlier launches on the same stream, so no workgroup of this launch waits
-// on another.  Halving each chain halves the latency it needs to hide: a
-// chain lane beside the block waves runs ~3x slower than alone.
-template <int TILE>
-__global__ void __launch_bounds__(kThreads, 1)
-sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                          uint8_t* __restrict__ digests, const PadSchedule pad, const ChainJob j0,
-                          const ChainJob j1, const uint32_t wpf, const uint32_t wpp, const uint32_t poff) {
-  // Chain waves are spread one per workgroup: workgroup g < C runs chain
-  // wave g as its wave 0 (job 0's waves first) and block waves 3g..3g+2 as
-  // its waves 1-3; the other workgroups run 4 block waves each.  So no CU
-  // hosts more than one chain wave per workgroup, and the chains' scattered
-  // digest loads are spread over C CUs instead of C/4.
-  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t C = j0.waves + j1.waves;  // chain waves
-  const uint32_t g = blockIdx.x;
-  uint64_t bw;
-#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
-  // A/B only: four chain waves per workgroup (ceil(C/4) chain workgroups)
-  const uint32_t CW = (C + 3) / 4;
-  if (g < CW) {
-    const uint32_t ci = g * 4 + wid;
-    if (ci < j0.waves) chain_job(j0, ci);
-    else if (ci < C) chain_job(j1, ci - j0.waves);
-    return;
-  }
-  bw = (uint64_t)(g - CW) * kWavesPerWG + wid;
-#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
-  // A/B only: the mixed workgroups' block waves hash SF_CHAIN_UNITS units each
-  if (g < C) {
-    if (wid == 0) {
-      if (g < j0.waves) chain_job(j0, g);
-      else chain_job(j1, g - j0.waves);
-      return;
-    }
-    const uint64_t first = ((uint64_t)g * 3 + (wid - 1)) * SF_CHAIN_UNITS;
-    for (int k = 0; k < SF_CHAIN_UNITS; ++k) {
-      uint64_t u = first + k;
-      if (wpp != wpf) u = (uint64_t)((uint32_t)u / wpp) * wpf + poff + (uint32_t)u % wpp;
-      fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, u, smem + wid * 64 * (TILE / 16));
-    }
-    return;
-  }
-  bw = (uint64_t)C * 3 * SF_CHAIN_UNITS + (uint64_t)(g - C) * kWavesPerWG + wid;
-#else
-  if (g < C) {
-    if (wid == 0) {
-      if (g < j0.waves) chain_job(j0, g);
-      else chain_job(j1, g - j0.waves);
-      return;
-    }
-    bw = (uint64_t)g * 3 + (wid - 1);
-  } else {
-    bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
-  }
-#endif
-  // A column-range launch (wpp < wpf: every file's block waves [poff,
-  // poff + wpp) of its wpf) maps its wave bw to the file's wave.
-  if (wpp != wpf) bw = (uint64_t)((uint32_t)bw / wpp) * wpf + poff + (uint32_t)bw % wpp;
-  fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, bw, smem + wid * 64 * (TILE / 16));
-}
+// sha1_fixed_chained_kernel (a stream's batches with their chains) is in
+// sf_stream.hip, its own translation unit.
 
-#ifdef SF_TUNING
+#if defined(SF_TUNING) && !defined(SF_STREAM_TU)
 // Tuning variant: TWO blocks per lane (wave = 128 consecutive blocks; lane l
 // owns blocks l and 64 + l), 64-B LDS steps (8 KiB tile per wave), the two
 // compressions round-interleaved.  Fixed tiling, bs % 64 == 0, 16-B aligned
@@ -1044,6 +981,7 @@ __device__ __forceinline__ uint16_t length_class(uint32_t nch, uint32_t mbits) {
 
 // kmax: the largest key the sort looks at (blocks of a larger class share
 // it): 255 with 4 mantissa bits, so one 8-bit radix pass sorts the list.
+#ifndef SF_STREAM_TU
 __global__ void __launch_bounds__(256)
 table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __restrict__ keys,
                   uint32_t* __restrict__ idx, uint32_t mbits, uint32_t kmax) {
@@ -1053,6 +991,7 @@ table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __re
   keys[i] = (uint16_t)(k < kmax ? k : kmax);
   idx[i] = (uint32_t)i;
 }
+#endif
 
 // Wire emission of the signature table as the reference's FILE_BLOCK
 // messages (src/sync/ssh/proto.rs:162-166): "FILE_BLOCK\n" + 20 raw digest
@@ -1065,6 +1004,7 @@ __device__ __forceinline__ uint32_t dec_digits(uint64_t v) {
   return d;
 }
 
+#ifndef SF_STREAM_TU
 __global__ void __launch_bounds__(256)
 wire_file_blocks_kernel(const uint8_t* __restrict__ digests, uint64_t n, uint32_t block_size, uint32_t last_size,
                         uint8_t* __restrict__ out) {
@@ -1085,6 +1025,7 @@ wire_file_blocks_kernel(const uint8_t* __restrict__ digests, uint64_t n, uint32_
   for (int k = (int)nd - 1; k >= 0; --k) { o[32 + k] = (uint8_t)('0' + v % 10); v /= 10; }
   o[32 + nd] = '\n';
 }
+#endif
 
 // splitmix64 byte stream: word i = mix(seed + (i+1)*GAMMA),
 // little-endian; writes bytes [start, start+len) of the stream.
@@ -1095,6 +1036,7 @@ __device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t i) {
   return z ^ (z >> 31);
 }
 
+#ifndef SF_STREAM_TU
 __global__ void __launch_bounds__(256)
 fill_splitmix_kernel(uint8_t* __restrict__ out, uint64_t len, uint64_t seed, uint64_t start) {
   // Fast path: whole 16-B groups of 2 aligned stream words.
@@ -1118,6 +1060,7 @@ fill_splitmix_kernel(uint8_t* __restrict__ out, uint64_t len, uint64_t seed, uin
     }
   }
 }
+#endif
 
 
 }  // namespace sf
