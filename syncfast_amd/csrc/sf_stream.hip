@@ -38,34 +38,6 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
   const uint32_t C = j0.waves + j1.waves;  // chain waves
   const uint32_t g = blockIdx.x;
   uint64_t bw;
-#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
-  // A/B only: four chain waves per workgroup (ceil(C/4) chain workgroups)
-  const uint32_t CW = (C + 3) / 4;
-  if (g < CW) {
-    const uint32_t ci = g * 4 + wid;
-    if (ci < j0.waves) chain_job(j0, ci);
-    else if (ci < C) chain_job(j1, ci - j0.waves);
-    return;
-  }
-  bw = (uint64_t)(g - CW) * kWavesPerWG + wid;
-#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
-  // A/B only: the mixed workgroups' block waves hash SF_CHAIN_UNITS units each
-  if (g < C) {
-    if (wid == 0) {
-      if (g < j0.waves) chain_job(j0, g);
-      else chain_job(j1, g - j0.waves);
-      return;
-    }
-    const uint64_t first = ((uint64_t)g * 3 + (wid - 1)) * SF_CHAIN_UNITS;
-    for (int k = 0; k < SF_CHAIN_UNITS; ++k) {
-      uint64_t u = first + k;
-      if (wpp != wpf) u = (uint64_t)((uint32_t)u / wpp) * wpf + poff + (uint32_t)u % wpp;
-      fixed_wave<TILE, false>(data, len, bs, nblocks, digests, pad, nullptr, u, smem + wid * 64 * (TILE / 16));
-    }
-    return;
-  }
-  bw = (uint64_t)C * 3 * SF_CHAIN_UNITS + (uint64_t)(g - C) * kWavesPerWG + wid;
-#else
   if (g < C) {
     if (wid == 0) {
       if (g < j0.waves) chain_job(j0, g);
@@ -76,7 +48,6 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
   } else {
     bw = (uint64_t)C * 3 + (uint64_t)(g - C) * kWavesPerWG + wid;
   }
-#endif
   // A column-range launch (wpp < wpf: every file's block waves [poff,
   // poff + wpp) of its wpf) maps its wave bw to the file's wave.
   if (wpp != wpf) bw = (uint64_t)((uint32_t)bw / wpp) * wpf + poff + (uint32_t)bw % wpp;
@@ -93,15 +64,8 @@ int launch_chained(const uint8_t* data, uint64_t len, uint32_t bs, uint64_t nblo
   // grid: C mixed workgroups (1 chain wave + 3 block waves), then 4 block
   // waves per workgroup for the rest
   const uint64_t C = j0.waves + j1.waves;
-#if defined(SF_TUNING) && defined(SF_CHAIN_PACK4)
-  const unsigned grid = (unsigned)(ceil_div(C, 4) + ceil_div(bwaves, sf::kWavesPerWG));  // A/B only
-#elif defined(SF_TUNING) && defined(SF_CHAIN_UNITS)
-  const uint64_t rest = bwaves > 3 * C * SF_CHAIN_UNITS ? bwaves - 3 * C * SF_CHAIN_UNITS : 0;  // A/B only
-  const unsigned grid = (unsigned)(C + ceil_div(rest, sf::kWavesPerWG));
-#else
   const uint64_t rest = bwaves > 3 * C ? bwaves - 3 * C : 0;
   const unsigned grid = (unsigned)(C + ceil_div(rest, sf::kWavesPerWG));
-#endif
   if (grid == 0) return SF_OK;
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<128>, dim3(grid), dim3(sf::kThreads), 0, stream, data, len, bs,
                      nblocks, digests, pad, j0, j1, wpf, wpp, poff);
