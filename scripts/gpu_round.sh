@@ -17,10 +17,13 @@ run() {  # name timeout cmd...
 if [ -n "$PROBE" ]; then
   run valu_probe 300 ./scripts/valu_probe || exit $?
 fi
+rc=0
+if [ -z "$SKIP_BASE" ]; then  # SKIP_BASE=1: only the optional steps below
 run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 150 --timeout-method thread
 rc=$?; if [ $rc -ge 2 ]; then exit $rc; fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 600 python bench.py --steps "$STEPS" --warmup 2 --cpu-seconds 8 || exit $?
+fi
 if [ -n "$EXTRA" ]; then
   run bench_c3 600 python bench.py --config 3 --steps "$STEPS" --warmup 2 --no-cpu-baseline || exit $?
   run bench_c5 600 python bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline || exit $?
