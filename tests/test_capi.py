@@ -114,6 +114,42 @@ def test_struct_layout():
     assert ctypes.sizeof(_lib.BlockSig) == 32
     assert _lib.BlockSig.sha1.offset == 12
     assert ctypes.sizeof(_lib.FileDesc) == 16
+    assert ctypes.sizeof(_lib.ChainJob) == 40  # include/syncfast_amd.h sf_chain_job
+
+
+def test_chained_cols_validation_without_device():
+    # sf_index_device_batch_chained_cols checks its column range before any
+    # device work: whole 64-block waves of whole-wave files, lo < hi <= blocks
+    L = syncfast_amd.lib()
+    jobs = (_lib.ChainJob * 1)()
+
+    def call(nf, flen, bs, lo, hi, data=None, dig=None, nj=0):
+        return L.sf_index_device_batch_chained_cols(data, nf, flen, bs, lo, hi, dig, jobs, nj, None)
+
+    E = _lib.SF_EINVAL
+    assert call(2, 4096 * 128, 0, 0, 64) == E  # block size 0
+    assert call(2, 4096 * 96, 4096, 0, 64) == E  # 96 blocks per file: not whole waves
+    for lo, hi in [(0, 100), (32, 128), (64, 64), (128, 64), (0, 192)]:
+        assert call(2, 4096 * 128, 4096, lo, hi, 1 << 20, 1 << 20) == E, (lo, hi)
+    assert call(2, 4096 * 128, 4096, 0, 64) == E  # no data / digests
+    assert call(2, 4096 * 128, 4096, 0, 128, 1 << 20, 1 << 20, nj=3) == E  # at most two jobs
+    assert call(0, 4096 * 128, 4096, 0, 128) == 0  # nothing to hash, no jobs: nothing launched
+
+
+def test_batch_stream_column_split():
+    # BatchStream.push_last's cut: the first half of a chain (part 1) reads
+    # digests [0, ceil(64 * half / 20)), rounded up to whole 64-block waves
+    from syncfast_amd.device import BatchStream
+    assert BatchStream(1024, 8 << 20, 4096)._half_cols() == 1024
+    assert BatchStream(40, 128 * 4096, 4096)._half_cols() == 64
+    assert BatchStream(9, 192 * 1024, 1024)._half_cols() == 128
+    assert BatchStream(4, 64 * 4096, 4096)._half_cols() is None  # one wave per file
+    assert BatchStream(4, 100 * 4096, 4096)._half_cols() is None  # not whole waves
+    assert BatchStream(4, 1024 * 4096, 4096, split=False)._half_cols() is None
+    for nbf in range(128, 4097, 64):
+        cut = BatchStream(3, nbf * 4096, 4096)._half_cols()
+        half = (nbf * 20 // 64) // 2
+        assert cut is not None and cut % 64 == 0 and cut * 20 >= half * 64 and cut - 64 < -(-half * 64 // 20)
 
 
 def test_argument_validation_without_device():
