@@ -123,6 +123,21 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   return hip_err(hipGetLastError());
 }
 
+// CUs of the current device (cached).
+inline unsigned device_cus() {
+  static std::atomic<int> cached{0};
+  int v = cached.load();
+  if (v > 0) return (unsigned)v;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess ||
+      hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) {
+    (void)hipGetLastError();
+    return 64;  // conservative (a quarter of MI355X's CUs)
+  }
+  cached.store(v);
+  return (unsigned)v;
+}
+
 // Explicit block lists of at least this many blocks are hashed in order of
 // length (sha1_table_kernel's `order`): a wave runs as long as its longest
 // block, so 64 blocks of mixed sizes side by side waste most lanes -- a list
@@ -206,14 +221,19 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
   const unsigned grid = grid_for_blocks(nblocks);
   void* ws = nullptr;
   const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
+  // the critical-path test in sha1_table_kernel: a wave's length against
+  // the list's compressions (estimated) over the lanes of the device's
+  // resident waves (3 per SIMD)
+  const uint64_t work = len / 64 + nblocks;
+  const uint64_t lane_slots = 64ull * 4 * 3 * device_cus();
   if (weak)
     hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, true>), dim3(grid), dim3(sf::kThreads), 0, stream,
                        static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, weak, order);
+                       static_cast<uint8_t*>(d_digests), d_status, weak, order, work, lane_slots);
   else
     hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, false>), dim3(grid), dim3(sf::kThreads), 0, stream,
                        static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, nullptr, order);
+                       static_cast<uint8_t*>(d_digests), d_status, nullptr, order, work, lane_slots);
   const int rc = hip_err(hipGetLastError());
   if (ws) (void)hipFreeAsync(ws, stream);
   return rc;
@@ -234,19 +254,6 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
 // SF_ETIMEDOUT; with d_status == NULL the unstaged path is taken.
 // SF_TEST_CHAIN_SPIN_LIMIT (test hook) bounds the polls of each wait
 // (default 2^24, several seconds).
-inline unsigned device_cus() {
-  static std::atomic<int> cached{0};
-  int v = cached.load();
-  if (v > 0) return (unsigned)v;
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess ||
-      hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) {
-    (void)hipGetLastError();
-    return 64;  // conservative (a quarter of MI355X's CUs)
-  }
-  cached.store(v);
-  return (unsigned)v;
-}
 
 inline uint32_t chain_spin_limit() {
   const int64_t v = knob(K_TEST_CHAIN_SPIN_LIMIT);

@@ -901,11 +901,22 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
 // mixed sizes (content-defined blocks, files' short last blocks) wastes
 // most lanes unless each wave's 64 blocks are about the same length; and
 // handing out the longest blocks first keeps the grid's tail short (LPT).
+// Critical-path priority (`work`, with `order`; round 3).  The longest
+// waves start first, but at a third of their SIMD's issue they would still
+// be running after every short wave is done, then finish alone at a lone
+// wave's rate.  A wave whose length exceeds the list's average work per wave
+// slot (work / lane_slots, in compressions) is on that path, so it issues at
+// priority 2 and the short waves beside it fill the cycles its dependency
+// stalls leave: the CDC-like 4 GiB list 2933 -> 3035 GiB/s interleaved
+// (profiles/r03/cdc_prio/).  `work` is the launcher's estimate len / 64 +
+// nblocks (exact for a list that tiles the data once): summing the sizes
+// on the device took same-address atomics that cost more than the sort.
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(kThreads, 3)  // 3 waves/SIMD, as the fixed kernel (the weak form asked 169 VGPRs)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
-                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order) {
+                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
+                  uint64_t work, uint64_t lane_slots) {
   constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
   __shared__ uint4 smem[kWavesPerWG * kWaveTile];
   const int lane = threadIdx.x & 63;
@@ -938,6 +949,11 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
                ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
+#ifndef SF_TABLE_PRIO
+#define SF_TABLE_PRIO 1  // 0: no critical-path priority (A/B)
+#endif
+  if (SF_TABLE_PRIO && order && work && (uint64_t)geo.max_nch * lane_slots >= work)
+    __builtin_amdgcn_s_setprio(2);
 
   Sha1 st;
   Adler wk;
