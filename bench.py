@@ -31,6 +31,10 @@ Rank 0 prints ONE JSON line (contract in the task statement), with:
   e2e_host_buffer -- not `value`: the same bytes from a host buffer through
                    sf_index_buffer (H2D + kernel + D2H rows), beside the raw
                    pinned H2D rate (north_star asks for the end-to-end rate);
+  content_defined_list -- not `value`: the reference's default block shape
+                   (content-defined, mean 8 KiB, max 32 KiB) as an explicit
+                   4 GiB list through sf_index_device_blocks, beside the same
+                   bytes as a 4 KiB list (config 2 at N=1);
   config1       -- BASELINE configs[0] (the unmodified Rust CPU path): probed
                    live (cargo / rustc on this host) and reported as not
                    runnable when they are absent.
@@ -101,6 +105,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the end-to-end leg (the same bytes from a host buffer through sf_index_buffer)")
+    p.add_argument("--no-cdc-list", action="store_true",
+                   help="skip the content-defined-like list leg (config 2 at N=1: the reference's default block "
+                        "shape through the explicit-list kernel, not `value`)")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--gather-root", default="rotate", choices=("rotate", "fixed"),
                    help="rank that receives each step's tables: rotates over the ranks, the last step's being "
@@ -239,6 +246,69 @@ def cpu_model() -> str:
 
 
 E2E_MAX = 8 * GiB  # host RAM bound of the end-to-end leg (config 4 at 256 GiB per GPU would not fit)
+CDC_LIST_BYTES = 4 * GiB  # the content-defined-like list leg: scripts/cdc_ab.py's list
+
+
+def content_defined_list(torch, data, stream, rounds=7, reps=3):
+    """Not `value`: the reference's DEFAULT block shape, content-defined
+    blocks (cdchunking ZPAQ 13 bits, max 32 KiB, src/index.rs:40-41; the
+    boundaries themselves are the host crate's), as an
+    explicit list over the shard's first 4 GiB: geometric sizes (mean 8 KiB,
+    capped at 32 KiB, byte offsets; scripts/cdc_ab.py's list, seed 7) through
+    sf_index_device_blocks (length-class sort + sha1_table_kernel), against
+    the same bytes as a 4 KiB list through the same entry point, interleaved,
+    HIP events on the launch stream around each round of calls.  64 random
+    blocks checked with the product's host SHA-1."""
+    import statistics
+    import numpy as np
+    from syncfast_amd import device, host
+    total = min(CDC_LIST_BYTES, data.numel())
+    rng = np.random.default_rng(7)
+    sz = np.minimum(32768, np.maximum(1, rng.geometric(1 / 8192, size=total // 4096 + 64))).astype(np.int64)
+    c = np.cumsum(sz)
+    n = int(np.searchsorted(c, total))
+    sz = sz[: n + 1]
+    sz[-1] -= int(c[n] - total) if c[n] > total else 0
+    sz = sz[sz > 0]
+    offs = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.int64)
+    o4 = np.arange(total // 4096, dtype=np.int64) * 4096
+    view = data[:total]
+    lists = {"cdc": (offs, sz), "list4k": (o4, np.full(o4.size, 4096, np.int64))}
+    dl = {k: (torch.from_numpy(o).to(data.device), torch.from_numpy(z.astype(np.int32)).to(data.device))
+          for k, (o, z) in lists.items()}
+    outs = {k: torch.empty((lists[k][0].size, 20), dtype=torch.uint8, device=data.device) for k in lists}
+
+    def run(k):
+        device.index_device_blocks(view, dl[k][0], dl[k][1], out=outs[k], check_range=False, stream=stream)
+
+    for k in lists:
+        run(k)
+    t_ramp = time.perf_counter()  # the GPU idled through the self-checks: clock back up first
+    while time.perf_counter() - t_ramp < 0.3:
+        run("list4k")
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    times = {k: [] for k in lists}
+    for r in range(rounds):
+        for k in (lists if r % 2 == 0 else reversed(list(lists))):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                run(k)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) / reps)
+    d = outs["cdc"].cpu().numpy()
+    for j in list(rng.integers(0, offs.size, 64)) + [0, offs.size - 1]:
+        b = view[int(offs[j]): int(offs[j]) + int(sz[j])].cpu().numpy()
+        assert bytes(d[j]) == host.sha1(b), "content-defined list digest self-check failed"
+    med = {k: statistics.median(v) for k, v in times.items()}
+    gibs = {k: total / GiB / (med[k] * 1e-3) for k in med}
+    return {"bytes": total, "blocks": int(offs.size), "mean_block": round(total / offs.size, 1),
+            "ms_per_call": round(med["cdc"], 4), "GiB/s": round(gibs["cdc"], 1),
+            "list4k_GiB/s": round(gibs["list4k"], 1), "of_list4k": round(gibs["cdc"] / gibs["list4k"], 4),
+            "entry": "sf_index_device_blocks (sort + sha1_table_kernel per call)",
+            "rounds": rounds, "reps": reps}
 
 
 def e2e_host_buffer(torch, data, dig_host, bs):
@@ -572,6 +642,9 @@ def main():
             traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
+    cdc = None
+    if not a.no_cdc_list and world == 1 and files is None and weaks is None and a.config == 2:
+        cdc = content_defined_list(torch, data, stream)
     e2e = None
     if not a.no_e2e and world == 1 and files is None and weaks is None:
         e2e = e2e_host_buffer(torch, data, d, bs)
@@ -631,6 +704,7 @@ def main():
         "hbm_frac_of_peak": round(total_bytes / world / (t / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
         "e2e_host_buffer": e2e,
+        "content_defined_list": cdc,
     }
     print(json.dumps(line), flush=True)
     if distributed:
