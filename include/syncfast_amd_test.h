@@ -31,6 +31,13 @@ int sf_test_get_knob(const char* name, int64_t* value);
  *                       memory): those are copied through the pinned stages. */
 int sf_test_get_stat(const char* name, int64_t* value);
 
+/* The processing order sha1_table_kernel gets for a sorted explicit list:
+ * d_order[0, n) (device uint32) receives the block indices ordered by
+ * length class (4 mantissa bits, 8-bit key), descending, list order within
+ * a class -- the counting sort of sf_sort.hip.  d_sizes: n device uint32.
+ * Asynchronous on `stream`; SF_EINVAL for n >= 2^32. */
+int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,8 +36,9 @@ EXPORTED = (
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
-# Test hooks (include/syncfast_amd_test.h): knobs latched at load, route counters.
-EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat")
+# Test hooks (include/syncfast_amd_test.h): knobs latched at load, route counters,
+# the explicit-list processing order.
+EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat", "sf_test_table_order")
 
 
 class SfError(OSError):
@@ -110,6 +111,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_test_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_int64, pi64]
     L.sf_test_get_knob.argtypes = [ctypes.c_char_p, pi64]
     L.sf_test_get_stat.argtypes = [ctypes.c_char_p, pi64]
+    L.sf_test_table_order.argtypes = [vp, u64, vp, vp]
     for name in EXPORTED + EXPORTED_TEST:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int

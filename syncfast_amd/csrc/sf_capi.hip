@@ -154,12 +154,15 @@ inline uint64_t table_sort_min() {
 constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
 
 // Stream-ordered workspace holding the processing order of blocks [0, n) of
-// a list: stable radix sort of (length class, index) by class, descending,
-// with rocprim on `s` (list order within a class).  Stability matters: a
-// wave's 64 blocks are then alike in length AND close together in memory; a
-// class-bucketing by atomics (three small launches instead of the sort's
-// ~70 us) scattered each class's blocks across the buffer and the list ran
+// a list: stable sort of the blocks by length class, descending, on `s`
+// (list order within a class).  Stability matters: a wave's 64 blocks are
+// then alike in length AND close together in memory; a class-bucketing by
+// atomics scattered each class's blocks across the buffer and the list ran
 // at half the rate (1410 vs 2609 GiB/s on one box, profiles/r03/bucket_sort_rejected/).
+// The default 8-bit key takes the counting sort of sf_sort.hip (three
+// kernels, ~21 us for 0.5 M blocks, against ~56 us of GPU time for rocprim's
+// radix sort with its key kernel; profiles/r03/sort/); wider keys (the
+// SF_TABLE_CLASS_BITS A/B knob) keep rocprim.
 // Returns nullptr (unsorted launch) if anything fails.
 uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
   *ws_out = nullptr;
@@ -174,6 +177,25 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   const unsigned kbits = mbits <= 4 ? 8u : 5u + mbits;
   const uint32_t kmax = (1u << kbits) - 1u;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+#ifndef SF_CLASS_SORT
+#define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
+#endif
+  if (SF_CLASS_SORT && kbits == 8) {  // the default: one counting pass over 256 classes (sf_sort.hip)
+    const size_t ob = up(n * 4), total = ob + up(sfi::class_order_workspace(n));
+    uint8_t* ws = nullptr;
+    if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    uint32_t* order = reinterpret_cast<uint32_t*>(ws);
+    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, s) != SF_OK) {
+      (void)hipGetLastError();
+      (void)hipFreeAsync(ws, s);
+      return nullptr;
+    }
+    *ws_out = ws;
+    return order;
+  }
   uint16_t *kin = nullptr, *kout = nullptr;
   uint32_t *iin = nullptr, *iout = nullptr;
   size_t tmp = 0;

@@ -261,4 +261,12 @@ inline unsigned io_threads() {
   return v > 0 ? (unsigned)std::min<int64_t>(v, 64) : 16u;
 }
 
+// Processing order of an explicit block list (sf_sort.hip): d_order[0, n)
+// receives the block indices sorted by 8-bit length class (kmax <= 255),
+// descending, list order within a class.  d_ws: class_order_workspace(n)
+// bytes of device memory.  Stream-ordered on s.
+size_t class_order_workspace(uint64_t n);
+int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
+                hipStream_t s);
+
 }  // namespace sfi

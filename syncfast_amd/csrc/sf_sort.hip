@@ -1,0 +1,179 @@
+// sf_sort.hip -- the processing order of an explicit block list for
+// sha1_table_kernel: a stable counting sort of the
+// blocks by their 8-bit length class, descending (list order within a
+// class), in three small kernels.  It replaces a general radix sort that
+// spent ~45 us per call (key kernel, three buffer fills, histogram and
+// onesweep passes) on what is one pass over 256 bins.
+//
+// Its own translation unit, so that it cannot change how sf_capi.hip's
+// block kernels compile.
+#define SF_STREAM_TU 1  // the device functions of sf_kernels.hpp only
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sf_internal.hpp"
+#include "sf_kernels.hpp"
+#include "../../include/syncfast_amd_test.h"
+
+namespace sf {
+
+constexpr int kSortThreads = 256;
+constexpr int kSortRounds = 8;
+constexpr uint32_t kSortTile = kSortThreads * kSortRounds;  // blocks per tile
+constexpr uint32_t kSortBins = 256;                          // 8-bit class keys
+
+__device__ __forceinline__ uint32_t class_key(uint32_t size, uint32_t mbits, uint32_t kmax) {
+  const uint32_t k = length_class(n_chunks(size), mbits);
+  return k < kmax ? k : kmax;
+}
+
+// Inclusive scan of v over the 256 threads of the workgroup; *total = the sum.
+__device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, m, 64);
+    if (lane >= m) v += o;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (int i = 0; i < kSortThreads / 64; ++i)
+    if (i < w) before += wsum[i];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();  // wsum is reused by the next call
+  return v + before;
+}
+
+// 1. Class histogram of every tile, bin-major: hist[bin * ntiles + tile].
+__global__ void __launch_bounds__(kSortThreads)
+class_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t kmax,
+                  uint32_t* __restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t h[kSortBins];
+  const uint32_t tid = threadIdx.x, tile = blockIdx.x;
+  h[tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)tile * kSortTile;
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortThreads + tid;
+    if (i < n) atomicAdd(&h[class_key(sizes[i], mbits, kmax)], 1u);
+  }
+  __syncthreads();
+  hist[(uint64_t)tid * ntiles + tile] = h[tid];
+}
+
+// 2. Per bin (one workgroup each): exclusive prefix over the tiles, in
+// place, and the bin's total.
+__global__ void __launch_bounds__(kSortThreads)
+class_scan_kernel(uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ totals) {
+  __shared__ uint32_t wsum[kSortThreads / 64];
+  uint32_t* col = hist + (uint64_t)blockIdx.x * ntiles;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < ntiles; t0 += kSortThreads) {
+    const uint32_t t = t0 + threadIdx.x;
+    const uint32_t v = t < ntiles ? col[t] : 0u;
+    uint32_t total;
+    const uint32_t incl = block_scan256(v, wsum, &total);
+    if (t < ntiles) col[t] = carry + incl - v;
+    carry += total;
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// 3. Scatter: block i goes to order[pos], pos = (blocks of higher classes)
+// + (blocks of its class in earlier tiles) + (its rank in its tile: earlier
+// rounds, earlier waves of its round, lower lanes of its wave).
+__global__ void __launch_bounds__(kSortThreads)
+class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t kmax,
+                     const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t ntiles,
+                     uint32_t* __restrict__ order) {
+  constexpr int kWaves = kSortThreads / 64;
+  __shared__ uint32_t running[kSortBins];
+  __shared__ uint32_t wcnt[kWaves][kSortBins];
+  __shared__ uint32_t wsum[kWaves];
+  const uint32_t tid = threadIdx.x, tile = blockIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  // classes in descending order: bin b starts after every bin above it
+  const uint32_t tb = totals[kSortBins - 1 - tid];  // thread t holds bin 255 - t
+  uint32_t all;
+  const uint32_t above = block_scan256(tb, wsum, &all) - tb;
+  running[kSortBins - 1 - tid] = above + hist[(uint64_t)(kSortBins - 1 - tid) * ntiles + tile];
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) wcnt[i][tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)tile * kSortTile;
+  const uint64_t lt = (1ull << lane) - 1ull;  // lanes below this one
+  for (int r = 0; r < kSortRounds; ++r) {
+    const uint64_t i = base + (uint64_t)r * kSortThreads + tid;
+    const bool valid = i < n;
+    const uint32_t k = valid ? class_key(sizes[i], mbits, kmax) : 0u;
+    // lanes of this wave holding the same key: AND of 8 bit-plane ballots
+    uint64_t eq = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t m = __ballot((k >> b) & 1u);
+      eq &= ((k >> b) & 1u) ? m : ~m;
+    }
+    const uint32_t lower = (uint32_t)__popcll(eq & lt);
+    const bool leader = valid && lower == 0;
+    if (leader) wcnt[w][k] = (uint32_t)__popcll(eq);
+    __syncthreads();
+    uint32_t pos = 0;
+    if (valid) {
+      pos = running[k] + lower;
+      for (int v = 0; v < w; ++v) pos += wcnt[v][k];
+    }
+    __syncthreads();  // every lane has read running / wcnt
+    {
+      uint32_t add = 0;
+#pragma unroll
+      for (int v = 0; v < kWaves; ++v) {
+        add += wcnt[v][tid];
+        wcnt[v][tid] = 0;
+      }
+      running[tid] += add;
+    }
+    __syncthreads();
+    if (valid) order[pos] = (uint32_t)i;
+  }
+}
+
+}  // namespace sf
+
+namespace sfi {
+
+size_t class_order_workspace(uint64_t n) {
+  const uint64_t ntiles = (n + sf::kSortTile - 1) / sf::kSortTile;
+  return (size_t)(ntiles * sf::kSortBins + sf::kSortBins) * 4;
+}
+
+int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
+                hipStream_t s) {
+  if (n == 0) return SF_OK;
+  if (n > 0xFFFFFFFFull || kmax >= sf::kSortBins) return SF_EINVAL;
+  const uint32_t ntiles = (uint32_t)((n + sf::kSortTile - 1) / sf::kSortTile);
+  uint32_t* hist = static_cast<uint32_t*>(d_ws);
+  uint32_t* totals = hist + (uint64_t)ntiles * sf::kSortBins;
+  hipLaunchKernelGGL(sf::class_hist_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
+                     hist, ntiles);
+  hipLaunchKernelGGL(sf::class_scan_kernel, dim3(sf::kSortBins), dim3(sf::kSortThreads), 0, s, hist, ntiles,
+                     totals);
+  hipLaunchKernelGGL(sf::class_scatter_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
+                     hist, totals, ntiles, d_order);
+  return hip_err(hipGetLastError());
+}
+
+}  // namespace sfi
+
+extern "C" int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream) {
+  if (n == 0) return SF_OK;
+  if (!d_sizes || !d_order || n > 0xFFFFFFFFull) return SF_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  void* ws = nullptr;
+  if (hipMallocAsync(&ws, sfi::class_order_workspace(n), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
+  const int rc = sfi::class_order(d_sizes, n, 4, 255, ws, d_order, s);
+  (void)hipFreeAsync(ws, s);
+  return rc;
+}

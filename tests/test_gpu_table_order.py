@@ -159,3 +159,33 @@ def test_default_sort_large_cdc_list(gpu, knobs):
     knobs.set("SF_TEST_TABLE_SORT", 0)
     assert np.array_equal(got, device.index_device_blocks(t, to, tz).cpu().numpy())
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
+
+
+def _class_keys(sizes):
+    """length_class(n_chunks(size), 4 mantissa bits) clamped at 255
+    (sf_kernels.hpp), in numpy."""
+    nch = (sizes.astype(np.int64) + 8) // 64 + 1
+    e = np.floor(np.log2(nch)).astype(np.int64)
+    k = np.where(nch < 16, nch, (e << 4) + ((nch >> np.maximum(e - 4, 0)) & 15))
+    return np.minimum(k, 255)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 2047, 2048, 2049, 100_000, 1 << 20])
+def test_class_order_is_the_stable_descending_class_sort(gpu, n):
+    # the counting sort behind sha1_table_kernel's `order` (sf_sort.hip):
+    # classes descending, list order within a class, a permutation of [0, n)
+    import ctypes
+
+    from syncfast_amd._lib import check, lib
+    rng = np.random.default_rng(38_000 + n)
+    sizes = np.concatenate([rng.geometric(1 / 8192, n // 2), rng.integers(0, 1 << 31, n - n // 2)])
+    sizes = rng.permutation(np.minimum(sizes, (1 << 31) - 1)).astype(np.uint32)
+    sizes[: min(n, 5)] = [0, 1, 55, 56, (1 << 31) - 1][: min(n, 5)]
+    ts = torch.from_numpy(sizes.view(np.int32)).to(gpu)
+    order = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    check(lib().sf_test_table_order(ts.data_ptr(), n, order.data_ptr(),
+                                    ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)),
+          "sf_test_table_order")
+    got = order.cpu().numpy().view(np.uint32)
+    want = np.argsort(-_class_keys(sizes), kind="stable")
+    assert np.array_equal(got, want)
