@@ -14,7 +14,10 @@ Each library is loaded with ctypes; rounds are interleaved, every digest of
 every library must agree with the first, and the cdc list is spot-checked
 against hashlib.  CDC_ROUNDS (default 6) rounds of CDC_REPS (5) launches.
 CDC_ONLY=1 runs only the cdc list (rocprof passes); CDC_LISTS=list4k (or
-cdc,list4k) picks the lists, without the fixed-kernel reference point.
+cdc,list4k) picks the lists, without the fixed-kernel reference point;
+cdc16 = the cdc sizes with every block 16-B aligned (the aligned LDS path);
+a8k / u8k = equal 8 KiB blocks at 16-B aligned / byte offsets (stride 8195).
+GiB/s are of the bytes each list covers.
 """
 import ctypes
 import hashlib
@@ -71,6 +74,15 @@ def main():
     sz = cdc_sizes(total, rng)
     offs = np.concatenate([[0], np.cumsum(sz)[:-1]]).astype(np.int64)
     lists = {"cdc": (offs, sz)}
+    if "cdc16" in pick:  # the same sizes, every block 16-B aligned (gaps of < 16 B; blocks past 4 GiB dropped)
+        o16 = np.zeros_like(offs)
+        o16[1:] = (np.cumsum((sz[:-1] + 15) // 16 * 16))
+        keep = o16 + sz <= total
+        lists["cdc16"] = (o16[keep], sz[keep])
+    for name, stride in (("a8k", 8192), ("u8k", 8195)):  # equal 8 KiB blocks: aligned / byte offsets
+        if name in pick:
+            o = np.arange((total - 8192) // stride + 1, dtype=np.int64) * stride
+            lists[name] = (o, np.full(o.size, 8192, np.int64))
     if not only or "list4k" in pick:
         o4 = np.arange(total // 4096, dtype=np.int64) * 4096
         lists["list4k"] = (o4, np.full(o4.size, 4096, np.int64))
@@ -123,12 +135,14 @@ def main():
             b = data[int(offs[j]): int(offs[j]) + int(sz[j])].cpu().numpy().tobytes()
             assert bytes(d[j]) == hashlib.sha1(b).digest(), j
     res = {"blocks": {k: int(lists[k][0].size) for k in lists}, "bytes": total,
+           "list_bytes": {k: int(lists[k][1].sum()) for k in lists},
            "mean_block": round(total / offs.size, 1)}
     for i, p in enumerate(libs):
         for k in names:
             med = statistics.median(times[(i, k)])
+            nb = int(lists[k][1].sum()) if k in lists else total
             res[f"{os.path.basename(p)}:{k}"] = {"ms": round(med, 4), "min_ms": round(min(times[(i, k)]), 4),
-                                                 "GiB/s": round(total / GiB / (med * 1e-3), 1)}
+                                                 "GiB/s": round(nb / GiB / (med * 1e-3), 1)}
     print(json.dumps(res), flush=True)
 
 

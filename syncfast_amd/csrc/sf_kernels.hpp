@@ -959,10 +959,15 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   Adler wk;
   uint4* tile = smem + wid * kWaveTile;
 #ifndef SF_LIST_ALIGNED_TOO
-#define SF_LIST_ALIGNED_TOO 0  // 1: 16-B aligned waves take the 144-B slot path too (A/B)
+#define SF_LIST_ALIGNED_TOO 0  // 1: every 16-B aligned wave takes the 144-B slot path too (A/B)
 #endif
+  // The slot path also takes aligned waves whose blocks differ in size: the
+  // aligned path stages only the wave's shortest block's chunks through LDS
+  // and loads the rest per lane (a CDC-like list laid out 16-B aligned: 2772
+  // GiB/s that way, 3045 through the slots; equal 8 KiB blocks: 3165 aligned,
+  // 3138 at byte offsets through the slots; profiles/r03/cdcx/).
   const uint64_t lo16 = lo & ~15ull;
-  const bool list_path = !WEAK && (SF_LIST_ALIGNED_TOO || !geo.lds_ok) &&
+  const bool list_path = !WEAK && (SF_LIST_ALIGNED_TOO || !geo.lds_ok || geo.min_size != geo.max_size) &&
                          ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && hi - lo16 < 0xF0000000ull;
   if (list_path)
     hash_wave_list(data, off, size, valid, lo16, hi - lo16, tile, st);
