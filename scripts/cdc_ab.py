@@ -16,7 +16,9 @@ against hashlib.  CDC_ROUNDS (default 6) rounds of CDC_REPS (5) launches.
 CDC_ONLY=1 runs only the cdc list (rocprof passes); CDC_LISTS=list4k (or
 cdc,list4k) picks the lists, without the fixed-kernel reference point;
 cdc16 = the cdc sizes with every block 16-B aligned (the aligned LDS path);
-a8k / u8k = equal 8 KiB blocks at 16-B aligned / byte offsets (stride 8195).
+a8k / u8k = equal 8 KiB blocks at 16-B aligned / byte offsets (stride 8195);
+files = a ragged many-file batch (files of 0..200 KiB in 4 KiB blocks, each
+file's last block short, 16-B aligned file starts).
 GiB/s are of the bytes each list covers.
 """
 import ctypes
@@ -83,6 +85,14 @@ def main():
         if name in pick:
             o = np.arange((total - 8192) // stride + 1, dtype=np.int64) * stride
             lists[name] = (o, np.full(o.size, 8192, np.int64))
+    if "files" in pick:  # a ragged many-file batch: files of 0..200 KiB in 4 KiB blocks, 16-B aligned starts
+        fl = rng.integers(0, 200 * 1024, total // (100 * 1024) + 16)
+        starts = np.concatenate([[0], np.cumsum((fl + 15) // 16 * 16)[:-1]])
+        fl, starts = fl[starts + fl <= total], starts[starts + fl <= total]
+        nb = (fl + 4095) // 4096
+        fo = np.repeat(starts, nb) + 4096 * (np.arange(int(nb.sum())) - np.repeat(np.cumsum(nb) - nb, nb))
+        fz = np.minimum(4096, np.repeat(starts + fl, nb) - fo)
+        lists["files"] = (fo.astype(np.int64), fz.astype(np.int64))
     if not only or "list4k" in pick:
         o4 = np.arange(total // 4096, dtype=np.int64) * 4096
         lists["list4k"] = (o4, np.full(o4.size, 4096, np.int64))
