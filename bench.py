@@ -304,8 +304,10 @@ def content_defined_list(torch, data, stream, rounds=7, reps=3):
         assert bytes(d[j]) == host.sha1(b), "content-defined list digest self-check failed"
     med = {k: statistics.median(v) for k, v in times.items()}
     gibs = {k: total / GiB / (med[k] * 1e-3) for k in med}
+    alg = total + 20 * int(offs.size)  # every byte read once, 20 B written per block (per call)
     return {"bytes": total, "blocks": int(offs.size), "mean_block": round(total / offs.size, 1),
             "ms_per_call": round(med["cdc"], 4), "GiB/s": round(gibs["cdc"], 1),
+            "hbm_frac": round(alg / (med["cdc"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "list4k_GiB/s": round(gibs["list4k"], 1), "of_list4k": round(gibs["cdc"] / gibs["list4k"], 4),
             "entry": "sf_index_device_blocks (sort + sha1_table_kernel per call)",
             "rounds": rounds, "reps": reps}
