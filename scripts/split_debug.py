@@ -1,3 +1,12 @@
+"""Which blocks of one wave a library build hashes wrongly (probe, not a
+test): four 64-block explicit lists (16-B aligned, equal line offsets,
+random byte offsets) through sf_index_device_blocks of the library given as
+argv[1], each digest against hashlib; prints the bad blocks with off & 3,
+the line offset and the size.  Used to find the divergent-shuffle bug of the
+rejected last-touch layout (profiles/r03/cdc_prio/split_debug_*.log).
+
+usage: python scripts/split_debug.py path/to/libsyncfast_amd.so
+"""
 import ctypes, os, sys, numpy as np, torch
 sys.path.insert(0, os.getcwd())
 from syncfast_amd import device
