@@ -516,66 +516,73 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 }
 #endif
 
-// Deep-prefetch form of sha1_stream_range for chains that run beside a
-// streaming block launch (their digest loads miss to HBM under load): D
-// chunks (D x 64 B per lane) stay in flight.  nch is wave-uniform (every
-// file of a batch has the same run length); q must be 16-B aligned.
-template <int D>
-__device__ __forceinline__ void sha1_stream_deep(Sha1& st, const uint4* __restrict__ q, uint32_t nch) {
-  static_assert(D % 2 == 0, "chunks are refilled in pairs");
-  if (nch == 0) return;
-  uint4 buf[D][4];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    const uint32_t c = (uint32_t)k < nch ? (uint32_t)k : nch - 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)c * 4 + i];
+#ifndef SF_CHAIN_PRIO
+#define SF_CHAIN_PRIO 3  // wave priority of the stream's chain waves (A/B: make variant EXTRA=-DSF_CHAIN_PRIO=0)
+#endif
+// A stream's chain job on the chain wave of a block launch (wave 0 of one
+// of the first workgroups, sha1_fixed_chained_kernel).  Its digest loads are
+// staged through the workgroup's LDS tile (unused by a chain wave
+// otherwise), as the block waves stage theirs: per step, 8 DMA
+// wave-instructions each move whole 128-B lines of 8 files, so one
+// instruction touches 8 lines instead of the 64 that a lane-per-file load
+// touches.  The lane-per-file loads (4 chunks in flight per lane) cost the
+// launch 0.050 ms per batch of chains, the staged form 0.032 (config 3
+// launch sequence, profiles/r03/c3/seq/seq_chain_lds.txt).  Data chunks
+// [lo, hi) of each lane's run; part 0/2 then the padding chunk(s).
+__device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave, uint4* __restrict__ tile) {
+  __builtin_amdgcn_s_setprio(SF_CHAIN_PRIO);  // latency-bound chains issue first on a shared SIMD
+  const int lane = threadIdx.x & 63;
+  const uint32_t f = wave * 64 + lane;
+  const bool valid = f < j.files;
+  Sha1 st;
+  if (j.part == 2 && valid) {
+    const uint32_t* sv = reinterpret_cast<const uint32_t*>(j.state + (uint64_t)f * 20);
+    st.h0 = sv[0]; st.h1 = sv[1]; st.h2 = sv[2]; st.h3 = sv[3]; st.h4 = sv[4];
+  } else {
+    st.init();
   }
-  for (uint32_t c0 = 0; c0 < nch; c0 += D) {
+  const uint32_t n = j.hi - j.lo;                 // data chunks, uniform
+  const uint32_t nsteps = (n + 1) / 2;
+  const uint8_t* span_ptr = j.runs + (uint64_t)wave * 64 * j.run_len + (uint64_t)j.lo * 64;
+  const uint64_t files_here = j.files - wave * 64 < 64 ? j.files - wave * 64 : 64;
+  const uint64_t span = (files_here - 1) * j.run_len + (uint64_t)n * 64;
+  uint32_t voff[8];
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const uint32_t c = c0 + k;
-      if (c < nch) {
+  for (int q = 0; q < 8; ++q) {
+    const int b = q * 8 + lane / 8;  // file of the wave
+    const int s = lane % 8;
+    const int k = s ^ ((b >> 1) & 7);
+    voff[q] = (uint32_t)b * j.run_len + (uint32_t)k * 16u;
+  }
+  const int g = (lane >> 1) & 7;
+  const uint4* my = tile + lane * 8;
+  if (nsteps > 0) issue_step<128>(span_ptr, span, 0, voff, tile);
+  for (uint32_t t = 0; t < nsteps; ++t) {
+    uint4 raw[8];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 8; ++k) raw[k] = my[k ^ g];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nsteps) issue_step<128>(span_ptr, span, t + 1, voff, tile);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      if (2 * t + ch < n) {
         uint32_t w[16];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          w[4 * i + 0] = bswap32(buf[k][i].x);
-          w[4 * i + 1] = bswap32(buf[k][i].y);
-          w[4 * i + 2] = bswap32(buf[k][i].z);
-          w[4 * i + 3] = bswap32(buf[k][i].w);
-        }
-        // refill two chunks (one 128-B line) back to back after every
-        // second chunk, so each line of the run is fetched into L1 once
-        if (k & 1) {
-          const uint32_t n0 = c - 1 + D < nch ? c - 1 + D : nch - 1, n1 = c + D < nch ? c + D : nch - 1;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) buf[k - 1][i] = q[(uint64_t)n0 * 4 + i];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) buf[k][i] = q[(uint64_t)n1 * 4 + i];
+          w[4 * i + 0] = bswap32(raw[4 * ch + i].x);
+          w[4 * i + 1] = bswap32(raw[4 * ch + i].y);
+          w[4 * i + 2] = bswap32(raw[4 * ch + i].z);
+          w[4 * i + 3] = bswap32(raw[4 * ch + i].w);
         }
         st.compress(w);
       }
     }
   }
-}
-
-#ifndef SF_CHAIN_PRIO
-#define SF_CHAIN_PRIO 3  // wave priority of the stream's chain waves (A/B: make variant EXTRA=-DSF_CHAIN_PRIO=0)
-#endif
-__device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave) {
-  __builtin_amdgcn_s_setprio(SF_CHAIN_PRIO);  // latency-bound chains issue first on a shared SIMD
-  const uint32_t f = wave * 64 + (threadIdx.x & 63);
-  if (f >= j.files) return;
+  if (!valid) return;
   const uint8_t* p = j.runs + (uint64_t)f * j.run_len;
-  uint32_t* sv = reinterpret_cast<uint32_t*>(j.state + (uint64_t)f * 20);
-  Sha1 st;
-  if (j.part == 2) {
-    st.h0 = sv[0]; st.h1 = sv[1]; st.h2 = sv[2]; st.h3 = sv[3]; st.h4 = sv[4];
-  } else {
-    st.init();
-  }
-  sha1_stream_deep<SF_CHAIN_DEPTH>(st, reinterpret_cast<const uint4*>(p + (uint64_t)j.lo * 64), j.hi - j.lo);
   if (j.part == 1) {
+    uint32_t* sv = reinterpret_cast<uint32_t*>(j.state + (uint64_t)f * 20);
     sv[0] = st.h0; sv[1] = st.h1; sv[2] = st.h2; sv[3] = st.h3; sv[4] = st.h4;
     return;
   }

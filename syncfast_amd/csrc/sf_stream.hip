@@ -40,8 +40,8 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
   uint64_t bw;
   if (g < C) {
     if (wid == 0) {
-      if (g < j0.waves) chain_job(j0, g);
-      else chain_job(j1, g - j0.waves);
+      if (g < j0.waves) chain_job(j0, g, smem);
+      else chain_job(j1, g - j0.waves, smem);
       return;
     }
     bw = (uint64_t)g * 3 + (wid - 1);
