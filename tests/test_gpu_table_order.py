@@ -170,7 +170,7 @@ def _class_keys(sizes):
     return np.minimum(k, 255)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 2047, 2048, 2049, 100_000, 1 << 20])
+@pytest.mark.parametrize("n", [1, 63, 64, 2047, 2048, 2049, 100_000, 1 << 20, (1 << 23) + 77])
 def test_class_order_is_the_stable_descending_class_sort(gpu, n):
     # the counting sort behind sha1_table_kernel's `order` (sf_sort.hip):
     # classes descending, list order within a class, a permutation of [0, n)
@@ -187,5 +187,5 @@ def test_class_order_is_the_stable_descending_class_sort(gpu, n):
                                     ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)),
           "sf_test_table_order")
     got = order.cpu().numpy().view(np.uint32)
-    want = np.argsort(-_class_keys(sizes), kind="stable")
+    want = np.argsort((255 - _class_keys(sizes)).astype(np.uint8), kind="stable")  # descending, stable
     assert np.array_equal(got, want)
