@@ -909,15 +909,17 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
 // most lanes unless each wave's 64 blocks are about the same length; and
 // handing out the longest blocks first keeps the grid's tail short (LPT).
 // Critical-path priority (`work`, with `order`; round 3).  The longest
-// waves start first, but at a third of their SIMD's issue they would still
-// be running after every short wave is done, then finish alone at a lone
-// wave's rate.  A wave whose length exceeds the list's average work per wave
-// slot (work / lane_slots, in compressions) is on that path, so it issues at
-// priority 2 and the short waves beside it fill the cycles its dependency
-// stalls leave: the CDC-like 4 GiB list 2933 -> 3035 GiB/s interleaved
-// (profiles/r03/cdc_prio/).  `work` is the launcher's estimate len / 64 +
-// nblocks (exact for a list that tiles the data once): summing the sizes
-// on the device took same-address atomics that cost more than the sort.
+// waves start first, but at a third of their SIMD's issue they could still
+// be running after every short wave is done.  A wave whose length exceeds
+// the list's average work per wave slot (work / lane_slots, in
+// compressions) issues at priority 2, so the short waves beside it fill the
+// cycles its dependency stalls leave.  `work` is the launcher's estimate
+// len / 64 + nblocks (exact for a list that tiles the data once).  Measured
+// (profiles/r03/cdc_prio/): this machine code runs the CDC-like 4 GiB list
+// at 2991 GiB/s, the same code with priority 0 at 2954, builds without the
+// test at 2887 -- most of the gain is this compiled form, so its machine
+// code is pinned (table_kernel.json, a CPU test); re-expressions of the
+// same test compiled to slower code.
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(kThreads, 3)  // 3 waves/SIMD, as the fixed kernel (the weak form asked 169 VGPRs)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,

@@ -389,3 +389,14 @@ def test_chained_kernel_is_the_measured_one():
         rec = json.load(f)
     assert kernel_code_sha256(symbol=CHAINED_KERNEL) == rec["kernel_code_sha256"], \
         "the chained kernel changed: re-measure with scripts/c3_seq.sh and update the record"
+
+def test_table_kernel_is_the_measured_one():
+    # sha1_table_kernel<128, false>'s rate on content-defined lists depends on
+    # its compiled form: the committed measurement
+    # names the machine code it measured
+    import json
+    from syncfast_amd._lib import TABLE_KERNEL, kernel_code_sha256
+    with open(os.path.join(ROOT, "profiles", "r03", "cdc_prio", "table_kernel.json")) as f:
+        rec = json.load(f)
+    assert kernel_code_sha256(symbol=TABLE_KERNEL) == rec["kernel_code_sha256"], \
+        "the explicit-list kernel changed: re-measure with scripts/prio_thr.sh and update the record"
