@@ -248,15 +248,9 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
   // resident waves (3 per SIMD)
   const uint64_t work = len / 64 + nblocks;
   const uint64_t lane_slots = 64ull * 4 * 3 * device_cus();
-  if (weak)
-    hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, true>), dim3(grid), dim3(sf::kThreads), 0, stream,
-                       static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, weak, order, work, lane_slots);
-  else
-    hipLaunchKernelGGL((sf::sha1_table_kernel<kTile, false>), dim3(grid), dim3(sf::kThreads), 0, stream,
-                       static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes, nblocks,
-                       static_cast<uint8_t*>(d_digests), d_status, nullptr, order, work, lane_slots);
-  const int rc = hip_err(hipGetLastError());
+  const int rc = launch_table_kernel(weak != nullptr, grid, static_cast<const uint8_t*>(d_data), len, d_offsets,
+                                     d_sizes, nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order, work,
+                                     lane_slots, stream);
   if (ws) (void)hipFreeAsync(ws, stream);
   return rc;
 }

@@ -266,6 +266,12 @@ inline unsigned io_threads() {
 // descending, list order within a class.  d_ws: class_order_workspace(n)
 // bytes of device memory.  Stream-ordered on s.
 size_t class_order_workspace(uint64_t n);
+// sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
+// translation unit); SF_OK or the launch error.
+int launch_table_kernel(bool weak_form, unsigned grid, const uint8_t* d_data, uint64_t len,
+                        const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests,
+                        int* d_status, uint32_t* weak, const uint32_t* order, uint64_t work, uint64_t lane_slots,
+                        hipStream_t stream);
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
                 hipStream_t s);
 
