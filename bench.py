@@ -171,6 +171,26 @@ def multi_block(dist, torch, dev, a, rank, world, kern_ms, waits, roots, backend
                     "reading (HIP events around work.wait()), per gather, averaged"}
 
 
+def config_block(a, world):
+    """The line's `config` object: the workload string of BASELINE.json's
+    config, the per-GPU shard and the parallelism (one shard per rank, the
+    pipelined gather of the digest tables)."""
+    from syncfast_amd.shard import shard_range
+    cfg = CONFIGS[a.config]
+    bs = cfg["block"]
+    per_rank = int(a.shard_gib * GiB) if a.shard_gib else cfg["bytes"]
+    per_rank -= per_rank % bs
+    total = per_rank * world
+    shard = shard_range(total, bs, world, 0)[1]
+    gather = world > 1 and not a.no_gather
+    backend = "rccl" if a.dist_backend == "nccl" else a.dist_backend
+    return {"workload": cfg["workload"], "bytes_per_gpu": shard, "block_size": bs, "total_bytes": total,
+            "files": cfg["files"], "blocks": total // bs,
+            **({"c3_mode": a.c3_mode} if cfg["files"] > 1 else {}),
+            "parallelism": f"shard{world}" + (f"+{backend}_gather(pipelined, root %s)" % (
+                "rotating" if a.gather_root == "rotate" else "0") if gather else "")}
+
+
 def check_launch(a, world, rank) -> None:
     """CPU-only rehearsal of the N-rank launch (gloo): every rank joins, the
     world size is checked, and rank 0 prints the `multi` block built from
@@ -186,7 +206,7 @@ def check_launch(a, world, rank) -> None:
                         "gloo")
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item()),
-                          "multi": multi}), flush=True)
+                          "config": config_block(a, world), "multi": multi}), flush=True)
     dist.destroy_process_group()
 
 
@@ -211,7 +231,99 @@ def config1_probe():
             "probe": {**{k: (v or "absent") for k, v in tools.items()}, "~/.cargo": cargo_home},
             "note": None if runnable else "no Rust toolchain on this host; cpu_baseline times the C restatement "
                                           "(scalar, stands in for the sha1 0.6 crate) and cpu_baseline_shani the "
-                                          "SHA-NI host code on the same fixed tiling instead"}
+                                          "SHA-NI host code on the same fixed tiling instead; standin_cpu adds the "
+                                          "boundary finding with a stand-in chunker (same per-byte work, not the "
+                                          "crate's boundaries), default_mode_e2e the drop-in's default splice "
+                                          "with that chunker feeding sf_index_fd_blocks"}
+
+
+CONFIG1_BYTES = 64 << 20  # BASELINE configs[0]: one 64 MiB file (seed 0x5EED0000)
+
+
+def config1_standin(budget_s):
+    """configs[0]'s CPU cost with a STAND-IN chunker (no Rust toolchain, and
+    the crate's recurrence is unpinned): the ZPAQ-form
+    fragmenter of examples/zpaq_standin.h (13 bits, 32 KiB cap: the crate's
+    per-byte table lookup, compare, add and multiply -- NOT its boundaries)
+    over the 64 MiB file's bytes, alone and with every block SHA-1'd as it is
+    cut (the reference's single pass, src/index.rs:629-647; scalar SHA-1
+    standing in for the pure-Rust sha1 0.6 crate, and SHA-NI), one core, in
+    memory (SQLite and the file read excluded)."""
+    import oracle  # CPU baseline leg: the stand-in chunker + SHA-1 timed on the host
+    buf = oracle.splitmix_bytes(CONFIG1_BYTES, SEED)
+    res = {}
+    for name, fn in (("chunker", lambda: oracle.zpaq_standin_sizes(buf)),
+                     ("chunker_sha1_scalar", lambda: oracle.zpaq_standin_index(buf, False)),
+                     ("chunker_sha1_shani", lambda: oracle.zpaq_standin_index(buf, True))):
+        best, spent, reps = None, 0.0, 0
+        while reps < 2 or (spent < budget_s / 3 and reps < 20):
+            t0 = time.perf_counter()
+            n = len(fn())
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+            spent += dt
+            reps += 1
+        res[name] = {"GB/s": round(CONFIG1_BYTES / best / 1e9, 4), "ms": round(best * 1e3, 2), "reps": reps}
+        res["blocks"] = n
+    res.update({"bytes": CONFIG1_BYTES, "cores": 1, "kind": "stand-in",
+                "label": "stand-in: same per-byte work as cdchunking's ZPAQ (zpaq's fragmenter form, 13 bits, "
+                         "32 KiB cap), not the crate's boundaries; SHA-1 per block in the same pass",
+                "source": "examples/zpaq_standin.h via oracle/sf_baseline.cpp (sfb_zpaq_cut, sfb_zpaq_index)"})
+    return res
+
+
+def config1_default_mode_e2e():
+    """The drop-in's default mode end to end on configs[0]'s file (not
+    `value`): the 64 MiB file written to disk, then the plain-C consumer's -Z
+    splice (examples/build/sf_index: ONE open, the stand-in chunker streams the
+    open file in 64 KiB reads keeping the (offset, size) list, then
+    sf_index_fd_blocks hashes the list from the same descriptor on the GPU),
+    three passes in one process (the first pays the library's stage
+    allocations), each timed inside the consumer: chunker seconds + hashing
+    call seconds.  16 rows re-hashed with the product's host SHA-1."""
+    import random
+    import tempfile
+    from syncfast_amd import host
+    exe = os.path.join(ROOT, "examples", "build", "sf_index")
+    if not os.access(exe, os.X_OK):
+        return {"status": "examples/build/sf_index not built"}
+    import numpy as np
+    d = tempfile.mkdtemp(prefix="sf_cfg1_")
+    path = os.path.join(d, "file64m")
+    try:
+        import oracle  # input generation only (the same splitmix64 bytes as configs[0])
+        raw = oracle.splitmix_bytes(CONFIG1_BYTES, SEED).tobytes()
+        with open(path, "wb") as f:
+            f.write(raw)
+        r = subprocess.run([exe, "-Z", "-T", path, path, path], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"status": f"sf_index -Z failed ({r.returncode}): {r.stderr.strip()[-300:]}"}
+        times = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")]
+        rows = []
+        for ln in r.stdout.splitlines():
+            parts = ln.split()
+            if len(parts) == 3 and parts[0].isdigit():
+                rows.append((int(parts[0]), int(parts[1]), parts[2]))
+        nb = times[-1]["blocks"]
+        last = rows[-nb:]
+        assert sum(s for _o, s, _h in last) == CONFIG1_BYTES, "e2e rows do not tile the file"
+        for o, s, h in random.Random(7).sample(last, min(16, len(last))):
+            assert host.sha1(np.frombuffer(raw[o:o + s], np.uint8)).hex() == h, "e2e row self-check failed"
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+        os.rmdir(d)
+    best = min(times[1:] or times, key=lambda t: t["chunk_s"] + t["hash_s"])
+    c, h = best["chunk_s"], best["hash_s"]
+    return {"bytes": CONFIG1_BYTES, "blocks": nb, "passes": len(times),
+            "chunker_GB/s": round(CONFIG1_BYTES / c / 1e9, 4), "hash_call_GB/s": round(CONFIG1_BYTES / h / 1e9, 3),
+            "e2e_GB/s": round(CONFIG1_BYTES / (c + h) / 1e9, 4), "chunker_share": round(c / (c + h), 4),
+            "route": "file (page cache) -> stand-in chunker over the open fd (1 host core, 64 KiB reads) -> "
+                     "sf_index_fd_blocks on the same fd (pread windows, H2D, sha1_table_kernel, D2H rows + "
+                     "blocks_hash)",
+            "label": "stand-in chunker: the crate's per-byte work, not its boundaries"}
 
 
 def cpu_baseline(nbytes_total, bs, budget_s):
@@ -651,12 +763,15 @@ def main():
     if not a.no_e2e and world == 1 and files is None and weaks is None:
         e2e = e2e_host_buffer(torch, data, d, bs)
     cpu = cpu_all = cpu_ni = cpu_ni_all = None
+    config1 = config1_probe() if world == 1 else None
     if not a.no_cpu_baseline and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         cpu = cpu_baseline(shard, bs, a.cpu_seconds)
         cpu_all = cpu_baseline_all_cores(shard, bs, a.cpu_seconds / 4)
         cpu_ni = cpu_baseline_shani(shard, bs, a.cpu_seconds / 4, 1)
         cpu_ni_all = cpu_baseline_shani(shard, bs, a.cpu_seconds / 4, threads)
+        config1["standin_cpu"] = config1_standin(a.cpu_seconds / 4)
+        config1["default_mode_e2e"] = config1_default_mode_e2e()
 
     line = {
         "metric": "GiB/s indexed (device-resident), %d KiB blocks" % (bs // 1024)
@@ -672,13 +787,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes generated in HBM, seed 0x5EED0000)",
-        "config": {"workload": cfg["workload"], "bytes_per_gpu": shard, "block_size": bs,
-                   "total_bytes": total_bytes, "files": cfg["files"], "blocks": nblk * world,
-                   **({"c3_mode": a.c3_mode} if files else {}),
-                   "parallelism": f"shard{world}" + (f"+{'rccl' if a.dist_backend == 'nccl' else a.dist_backend}"
-                                                     "_gather(pipelined, root %s)" % (
-                                                         "rotating" if a.gather_root == "rotate" else "0")
-                                                     if gather else "")},
+        "config": config_block(a, world),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": ("sha1_fixed_chained_kernel<128>" if bstream is not None else
@@ -697,7 +806,7 @@ def main():
         "cpu_baseline_all_cores": cpu_all,
         "cpu_baseline_shani": cpu_ni,
         "cpu_baseline_shani_all_cores": cpu_ni_all,
-        "config1": config1_probe() if world == 1 else None,
+        "config1": config1,
         "lib_sha256": build,
         "code_object_sha256": kernels,
         "kernel_code_sha256": kcode,

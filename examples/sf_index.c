@@ -19,16 +19,25 @@
  *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
  *     -v N: the same bytes cut by the host chunker (-C), hashed as a list in
  *     HBM, the list's FILE_BLOCK run to stdout (sf_wire_blocks_fd);
- *     -L dst src: src's blocks looked up among dst's (sf_block_set_*)
+ *     -L dst src: src's blocks looked up among dst's (sf_block_set_*);
+ *     -Z: the drop-in's default splice: each file opened once, streamed
+ *     through a boundary chunker (the stand-in of zpaq_standin.h in place of
+ *     the cdchunking crate), its list hashed from the same descriptor
+ *     (sf_index_fd_blocks); -T adds a timing line per file on stderr.
+ * Regular files (default mode) go through the same one-open form:
+ * sf_file_stamp_fd + sf_index_fd_fixed on the open descriptor.
  */
+#include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "syncfast_amd.h"
+#include "zpaq_standin.h"
 
 /* -w only: device memory for the device-resident entry points (what a Rust
  * binding would take from hip-sys). */
@@ -56,28 +65,32 @@ static int print_rows(const char *name, const sf_block_sig *rows, uint64_t n, co
     return 0;
 }
 
+/* One open, as index_file (src/index.rs:615-625): the stamp (what the
+ * caller would take the mtime from) and the bytes come from the same
+ * descriptor; a file written while it is read gives SF_EAGAIN and is read
+ * again, at most 3 times. */
 static int index_one(const char *path, uint32_t bs) {
     uint8_t bh[20];
     struct stat sb;
     const int is_stdin = strcmp(path, "-") == 0;
-    if (!is_stdin && stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) {
-        uint64_t cap = sb.st_size ? ((uint64_t)sb.st_size + bs - 1) / bs : 0, n = 0;
-        sf_block_sig *rows = malloc((cap ? cap : 1) * sizeof(sf_block_sig));
-        if (!rows) return SF_ENOMEM;
-        int rc = sf_index_file(path, bs, rows, cap, &n, bh);
-        if (rc == SF_ENOSPC) {  /* the file grew since stat(): retry with the need */
-            sf_block_sig *more = realloc(rows, (n ? n : 1) * sizeof(sf_block_sig));
-            if (!more) { free(rows); return SF_ENOMEM; }
-            rows = more;
-            cap = n;
-            rc = sf_index_file(path, bs, rows, cap, &n, bh);
-        }
-        if (rc == SF_OK) print_rows(path, rows, n, bh);
-        free(rows);
-        return rc;
-    }
     const int fd = is_stdin ? 0 : open(path, O_RDONLY);
     if (fd < 0) return SF_EIO;
+    if (!is_stdin && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode)) {
+        int rc = SF_EAGAIN;
+        for (int attempt = 0; attempt < 3 && (rc == SF_EAGAIN || rc == SF_ENOSPC); attempt++) {
+            sf_file_stamp st;
+            uint64_t n = 0;
+            if ((rc = sf_file_stamp_fd(fd, &st)) != SF_OK) break;
+            const uint64_t cap = st.size ? (st.size + bs - 1) / bs : 0;
+            sf_block_sig *rows = malloc((cap ? cap : 1) * sizeof(sf_block_sig));
+            if (!rows) { rc = SF_ENOMEM; break; }
+            rc = sf_index_fd_fixed(fd, &st, bs, rows, cap, &n, bh);
+            if (rc == SF_OK) print_rows(path, rows, n, bh);
+            free(rows);
+        }
+        close(fd);
+        return rc;
+    }
     sf_block_sig *rows = NULL;
     uint64_t n = 0;
     const int rc = sf_index_fd(fd, bs, &rows, &n, bh);
@@ -191,6 +204,89 @@ static int index_cdc(const char *path) {
         free(again);
     }
     if (rc == SF_OK) print_rows(path, rows, n, bh);
+    free(buf);
+    free(offs);
+    free(sizes);
+    free(rows);
+    return rc;
+}
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* -Z: the drop-in's default splice from C (INTEGRATION.md
+ * index_file_rows_cdc): ONE open of the file and its stamp; the chunker
+ * streams the open file (64 KiB reads, as Chunker::stream reads it,
+ * src/index.rs:625) and only the (offset, size) list is kept; then
+ * sf_index_fd_blocks hashes the list from the same descriptor, so a file
+ * renamed over the path meanwhile changes nothing and one written in place
+ * gives SF_EAGAIN: cut again, at most 3 times.  The chunker is the stand-in
+ * of zpaq_standin.h (the crate's per-byte work, not its boundaries).  -T: one
+ * line per file on stderr, {"zpaq_file": ..., "bytes", "blocks", "chunk_s",
+ * "hash_s"}: the host chunker's time and the hashing call's. */
+static int index_zpaq(const char *path, int timing) {
+    enum { kRead = 1 << 16 };
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return SF_EIO;
+    uint8_t *buf = malloc(kRead), bh[20];
+    uint64_t n = 0, cap = 1024, total = 0, *offs = malloc(cap * sizeof(uint64_t));
+    uint32_t *sizes = malloc(cap * sizeof(uint32_t));
+    sf_block_sig *rows = NULL;
+    double t_chunk = 0, t_hash = 0;
+    int rc = (buf && offs && sizes) ? SF_EAGAIN : SF_ENOMEM;
+    for (int attempt = 0; attempt < 3 && rc == SF_EAGAIN; attempt++) {
+        sf_file_stamp st;
+        if ((rc = sf_file_stamp_fd(fd, &st)) != SF_OK) break;
+        if (lseek(fd, 0, SEEK_SET) != 0) { rc = SF_EIO; break; }
+        const double t0 = now_s();
+        sf_zpaq z;
+        sf_zpaq_init(&z, 13, 32768); /* ZPAQ_BITS, MAX_BLOCK_SIZE: src/index.rs:40-41 */
+        uint64_t start = 0;
+        n = total = 0;
+        for (int eof = 0; rc == SF_OK && !eof;) {
+            const ssize_t r = read(fd, buf, kRead);
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0) { rc = SF_EIO; break; }
+            uint64_t p = 0;
+            for (;;) { /* boundaries in this read; at EOF the open chunk ends (ChunkInput::End after data) */
+                const size_t k = r > 0 ? sf_zpaq_next(&z, buf + p, (size_t)((uint64_t)r - p)) : 0;
+                eof = r == 0;
+                if (k == 0 && !(eof && total > start)) break;
+                const uint64_t end = k ? total + p + k : total;
+                if (n == cap) {
+                    uint64_t *o2 = realloc(offs, 2 * cap * sizeof(uint64_t));
+                    if (o2) offs = o2;
+                    uint32_t *s2 = o2 ? realloc(sizes, 2 * cap * sizeof(uint32_t)) : NULL;
+                    if (s2) sizes = s2;
+                    if (!o2 || !s2) { rc = SF_ENOMEM; break; }
+                    cap *= 2;
+                }
+                offs[n] = start;
+                sizes[n++] = (uint32_t)(end - start);
+                start = end;
+                if (!k) break;
+                p += k;
+            }
+            total += r > 0 ? (uint64_t)r : 0;
+        }
+        t_chunk = now_s() - t0;
+        if (rc != SF_OK) break;
+        free(rows);
+        if (!(rows = malloc((n ? n : 1) * sizeof(sf_block_sig)))) { rc = SF_ENOMEM; break; }
+        const double t1 = now_s();
+        rc = sf_index_fd_blocks(fd, &st, offs, sizes, n, rows, bh);
+        t_hash = now_s() - t1;
+    }
+    close(fd);
+    if (rc == SF_OK) {
+        print_rows(path, rows, n, bh);
+        if (timing)
+            fprintf(stderr, "{\"zpaq_file\": \"%s\", \"bytes\": %llu, \"blocks\": %llu, \"chunk_s\": %.6f, \"hash_s\": %.6f}\n",
+                    path, (unsigned long long)total, (unsigned long long)n, t_chunk, t_hash);
+    }
     free(buf);
     free(offs);
     free(sizes);
@@ -332,7 +428,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0;
+    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -344,10 +440,12 @@ int main(int argc, char **argv) {
         else if (strcmp(argv[i], "-L") == 0) lookup = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
         else if (strcmp(argv[i], "-C") == 0) cdc = 1;
+        else if (strcmp(argv[i], "-Z") == 0) zpaq = 1;
+        else if (strcmp(argv[i], "-T") == 0) timing = 1;
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -s shards] path... | -w bytes | -v bytes | -L dst src\n",
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] | -s shards] path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
     }
@@ -382,7 +480,8 @@ int main(int argc, char **argv) {
         return status;
     }
     for (; i < argc; i++) {
-        const int rc = cdc ? index_cdc(argv[i])
+        const int rc = zpaq  ? index_zpaq(argv[i], timing)
+                       : cdc ? index_cdc(argv[i])
                        : (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)
                                                 : index_one(argv[i], bs);
         if (rc != SF_OK) {

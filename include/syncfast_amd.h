@@ -43,6 +43,7 @@ extern "C" {
 
 #define SF_OK 0
 #define SF_EIO (-5)      /* file read failed */
+#define SF_EAGAIN (-11)  /* the file changed under the call (fd routes): cut it again and retry */
 #define SF_ENOMEM (-12)  /* device, pinned or host allocation failed, or the system refused a thread */
 #define SF_ENODEV (-19)  /* no HIP device, or a HIP runtime error */
 #define SF_EINVAL (-22)  /* bad argument */
@@ -262,10 +263,56 @@ int sf_index_buffer_blocks(const uint8_t *data, uint64_t len, const uint64_t *of
  * src/index.rs:625), and the library reads each ~256 MiB window again with
  * pread (16 threads) into the pinned stages -- the file is never held whole
  * in memory.  List checked against the file's size first (SF_ERANGE /
- * SF_EINVAL as above); SF_EIO if it cannot be opened, is not a regular file
- * or shrinks while being read.  Rows in list order + blocks_hash; blocking. */
+ * SF_EINVAL as above); SF_EIO if it cannot be opened or is not a regular
+ * file; SF_EAGAIN if it changes while being read (stamps as in
+ * sf_index_fd_blocks).  Rows in list order + blocks_hash; blocking.
+ * The path is opened a second time here, after the chunker's open: a file
+ * renamed over the path in between is hashed with the old file's
+ * boundaries.  The drop-in splice uses sf_index_fd_blocks on the chunker's
+ * own descriptor instead. */
 int sf_index_file_blocks(const char *path, const uint64_t *offsets, const uint32_t *sizes,
                          uint64_t n_blocks, sf_block_sig *out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
+/* What fstat says about an open file's contents: the identity of the bytes a
+ * chunker read through that descriptor.  Two stamps match when dev, ino,
+ * size and mtime are equal and, unless the link count changed, ctime too:
+ * ctime moves on every write and cannot be set back by the writer (mtime
+ * can), but it also moves when a link is added or removed -- a file renamed
+ * over the path unlinks the open one, which changes nothing it holds.
+ * Timestamps are only as fine as the filesystem's clock tick: a write within
+ * the same tick as the stamp is not seen. */
+typedef struct sf_file_stamp {
+    uint64_t dev, ino, size, nlink;
+    int64_t mtime_sec, mtime_nsec;
+    int64_t ctime_sec, ctime_nsec;
+} sf_file_stamp;
+
+/* fstat(fd) as a stamp.  SF_EIO if fstat fails. */
+int sf_file_stamp_fd(int fd, sf_file_stamp *out);
+
+/* The explicit list over the regular file OPEN on fd -- the handle the caller's
+ * chunker just streamed (index_file opens the file once and takes the mtime,
+ * the boundaries and the bytes from that one handle, src/index.rs:615-625).
+ * Reads with pread only (the descriptor's position is not used or moved), by
+ * ~256 MiB windows as sf_index_file_blocks.  A rename over the path after the
+ * open changes nothing: the descriptor still reads the file the chunker cut.
+ * expect (may be NULL): the stamp taken before the chunker read the file
+ * (sf_file_stamp_fd); if the file's stamp differs when the call starts, or
+ * changes between then and the last window read (an in-place write, append
+ * or truncation), the call returns SF_EAGAIN and the rows are not valid: the
+ * caller takes a new stamp and cuts the file again.  SF_EINVAL if fd is not a
+ * regular file (a pipe cannot be read twice: use sf_index_buffer_blocks);
+ * SF_ERANGE / SF_EINVAL for the list as sf_index_file_blocks.  Blocking. */
+int sf_index_fd_blocks(int fd, const sf_file_stamp *expect, const uint64_t *offsets, const uint32_t *sizes,
+                       uint64_t n_blocks, sf_block_sig *out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
+/* Fixed tiling of the regular file open on fd, [0, size at the call), through
+ * the pread pipeline of sf_index_file, with the same stamp checks as
+ * sf_index_fd_blocks (SF_EAGAIN: the file changed; the rows are not valid).
+ * SF_ENOSPC with *n_out = the need when cap is too small (nothing is read).
+ * SF_EINVAL if fd is not a regular file (use sf_index_fd).  Blocking. */
+int sf_index_fd_fixed(int fd, const sf_file_stamp *expect, uint32_t block_size, sf_block_sig *out,
+                      uint64_t cap, uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
 
 /* End to end from a file on disk (the reference's input, src/index.rs:615):
  * pread into pinned buffers, overlapped H2D + kernel, D2H.  Writes the

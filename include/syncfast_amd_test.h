@@ -38,6 +38,14 @@ int sf_test_get_stat(const char* name, int64_t* value);
  * Asynchronous on `stream`; SF_EINVAL for n >= 2^32. */
 int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream);
 
+/* Called by the descriptor and path routes that pread a regular file
+ * (sf_index_fd_blocks, sf_index_fd_fixed, sf_index_file_blocks,
+ * sf_index_file) after each window has been read, on the calling thread,
+ * with the window's index: a test changes the file at a known point of a
+ * call.  NULL removes it.  Not synchronised with calls in flight. */
+typedef void (*sf_test_read_hook_fn)(void* arg, uint64_t window);
+int sf_test_set_read_hook(sf_test_read_hook_fn fn, void* arg);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,11 @@ def baseline_lib() -> ctypes.CDLL:
         L.sfb_index_fixed_shani.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                             ctypes.c_int]
         L.sfb_index_fixed_shani.restype = ctypes.c_uint64
+        L.sfb_zpaq_cut.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.sfb_zpaq_cut.restype = ctypes.c_uint64
+        L.sfb_zpaq_index.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_int]
+        L.sfb_zpaq_index.restype = ctypes.c_uint64
         _base = L
     return _base
 
@@ -131,6 +136,34 @@ def index_fixed_shani(data, block_size: int, threads: int = 1) -> np.ndarray:
     dig = np.zeros((n, 20), np.uint8)
     baseline_lib().sfb_index_fixed_shani(_ptr(a), a.size, block_size, _ptr(dig), threads)
     return dig
+
+
+def zpaq_standin_sizes(data) -> np.ndarray:
+    """Block sizes of the ZPAQ-form STAND-IN chunker (examples/zpaq_standin.h,
+    13 bits, 32 KiB cap): the crate's per-byte work for the configs[0]
+    baseline, not the reference's boundaries."""
+    a = _as_u8(data)
+    cap = a.size // 1024 + 16
+    out = np.zeros(cap, np.uint32)
+    n = int(baseline_lib().sfb_zpaq_cut(_ptr(a), a.size, _ptr(out), cap))
+    if n > cap:  # more than one block per KiB: cut again into a list that fits
+        out = np.zeros(n, np.uint32)
+        baseline_lib().sfb_zpaq_cut(_ptr(a), a.size, _ptr(out), n)
+    return out[:n]
+
+
+def zpaq_standin_index(data, shani: bool) -> np.ndarray:
+    """The stand-in chunker with each block SHA-1'd as it is cut, in one pass
+    (the reference's default index_file loop, src/index.rs:629-647), on the
+    calling thread: digests u8[n, 20]."""
+    a = _as_u8(data)
+    cap = a.size // 1024 + 16
+    dig = np.zeros((cap, 20), np.uint8)
+    n = int(baseline_lib().sfb_zpaq_index(_ptr(a), a.size, _ptr(dig), cap, int(shani)))
+    if n > cap:
+        dig = np.zeros((n, 20), np.uint8)
+        baseline_lib().sfb_zpaq_index(_ptr(a), a.size, _ptr(dig), n, int(shani))
+    return dig[:n]
 
 
 def has_shani() -> bool:

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../syncfast_amd/csrc/host_sha1.h"
+#include "../examples/zpaq_standin.h"
 
 extern "C" {
 
@@ -35,6 +36,44 @@ uint64_t sfb_index_fixed_shani(const uint8_t* data, uint64_t len, uint64_t bs, u
   for (uint64_t k = 1; k < t && k * per < n; k++) pool.emplace_back(run, k * per, std::min(n, (k + 1) * per));
   run(0, std::min(n, per));
   for (auto& th : pool) th.join();
+  return n;
+}
+
+// configs[0] stand-in (bench.py cpu_baseline's config1 block): the
+// reference's default index_file loop over a buffer -- a ZPAQ-form chunker
+// (examples/zpaq_standin.h: the crate's per-byte work, NOT its boundaries)
+// with ZPAQ_BITS = 13 and MAX_BLOCK_SIZE = 32768 (/root/reference/src/
+// index.rs:40-41).  sfb_zpaq_cut: the chunker alone, block sizes into
+// sizes[0, cap) (the count is returned even past cap).  sfb_zpaq_index: the
+// reference's single pass, each block SHA-1'd as it is cut
+// (src/index.rs:629-647), scalar (the stand-in for the pure-Rust sha1 0.6
+// crate) or SHA-NI; digests[0, cap).
+uint64_t sfb_zpaq_cut(const uint8_t* data, uint64_t len, uint32_t* sizes, uint64_t cap) {
+  sf_zpaq z;
+  sf_zpaq_init(&z, 13, 32768);
+  uint64_t n = 0, start = 0, p = 0;
+  while (p < len) {
+    const size_t k = sf_zpaq_next(&z, data + p, (size_t)(len - p));
+    const uint64_t end = k ? p + k : len;
+    if (n < cap) sizes[n] = (uint32_t)(end - start);
+    n++;
+    start = p = end;
+  }
+  return n;
+}
+
+uint64_t sfb_zpaq_index(const uint8_t* data, uint64_t len, uint8_t* digests, uint64_t cap, int shani) {
+  sf_zpaq z;
+  sf_zpaq_init(&z, 13, 32768);
+  uint64_t n = 0, p = 0;
+  while (p < len) {
+    const size_t k = sf_zpaq_next(&z, data + p, (size_t)(len - p));
+    const uint64_t end = k ? p + k : len;
+    uint8_t d[20];
+    sf_host_sha1_impl(data + p, end - p, n < cap ? digests + 20 * n : d, shani ? 0 : 1);
+    n++;
+    p = end;
+  }
   return n;
 }
 

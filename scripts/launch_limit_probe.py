@@ -1,7 +1,7 @@
 """What one HIP launch does past 2^32 work-items, and that the split launch
 does not: 1-B blocks over 4 GiB + 77 B (2^32 + 77 blocks, one lane each),
 hashed once with the launcher's split (default) and once with it disabled
-(SF_LAUNCH_MAX_BLOCKS = 2^40, one launch), each in its own process; every
+(SF_TEST_LAUNCH_MAX_BLOCKS = 2^40, one launch), each in its own process; every
 digest is compared with SHA-1 of its byte (profiles/r02/split/).
 
 usage: python scripts/launch_limit_probe.py           (parent)
@@ -33,7 +33,7 @@ def child():
         if nbad and first_bad is None:
             first_bad = a + int((~ok).nonzero()[0])
         bad += nbad
-    print(f"SF_LAUNCH_MAX_BLOCKS={os.environ.get('SF_LAUNCH_MAX_BLOCKS', 'default')}: {n} blocks, "
+    print(f"SF_TEST_LAUNCH_MAX_BLOCKS={os.environ.get('SF_TEST_LAUNCH_MAX_BLOCKS', 'default')}: {n} blocks, "
           f"{bad} wrong digests" + (f", first at block {first_bad}" if bad else ""), flush=True)
 
 
@@ -41,7 +41,7 @@ def main():
     for knob in (None, str(1 << 40)):
         env = dict(os.environ)
         if knob:
-            env["SF_LAUNCH_MAX_BLOCKS"] = knob
+            env["SF_TEST_LAUNCH_MAX_BLOCKS"] = knob
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
         print((r.stdout.strip() or "<no output>") + ("" if r.returncode == 0 else f" rc={r.returncode} {r.stderr[-400:]}"),
               flush=True)

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("SF_LIB") or os.path.join(_HERE, "lib", "libsyncfast_a
 
 SF_OK = 0
 SF_EIO = -5
+SF_EAGAIN = -11
 SF_ENOMEM = -12
 SF_ENODEV = -19
 SF_EINVAL = -22
@@ -32,13 +33,14 @@ EXPORTED = (
     "sf_index_device_fixed", "sf_index_device_blocks", "sf_index_device_batch",
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
     "sf_index_device_batch_chained_cols",
-    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
+    "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_file_stamp_fd", "sf_index_fd_blocks", "sf_index_fd_fixed", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
 # Test hooks (include/syncfast_amd_test.h): knobs latched at load, route counters,
 # the explicit-list processing order.
-EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat", "sf_test_table_order")
+EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat", "sf_test_table_order",
+                 "sf_test_set_read_hook")
 
 
 class SfError(OSError):
@@ -60,6 +62,24 @@ class ChainJob(ctypes.Structure):
     """sf_chain_job: one blocks_hash chain job of an earlier batch."""
     _fields_ = [("d_digests", ctypes.c_void_p), ("n_files", ctypes.c_uint32), ("part", ctypes.c_uint32),
                 ("blocks", ctypes.c_uint64), ("d_state", ctypes.c_void_p), ("d_hashes", ctypes.c_void_p)]
+
+
+class FileStamp(ctypes.Structure):
+    """sf_file_stamp: fstat's identity of an open file's contents."""
+    _fields_ = [("dev", ctypes.c_uint64), ("ino", ctypes.c_uint64), ("size", ctypes.c_uint64),
+                ("nlink", ctypes.c_uint64), ("mtime_sec", ctypes.c_int64), ("mtime_nsec", ctypes.c_int64),
+                ("ctime_sec", ctypes.c_int64), ("ctime_nsec", ctypes.c_int64)]
+
+
+def same_stamp(a: FileStamp, b: FileStamp) -> bool:
+    """The library's stamp comparison (include/syncfast_amd.h): dev, ino, size
+    and mtime equal, and ctime too unless the link count changed."""
+    return (a.dev, a.ino, a.size, a.mtime_sec, a.mtime_nsec) == (b.dev, b.ino, b.size, b.mtime_sec, b.mtime_nsec) \
+        and (a.nlink != b.nlink or (a.ctime_sec, a.ctime_nsec) == (b.ctime_sec, b.ctime_nsec))
+
+
+# sf_test_read_hook_fn: void (*)(void* arg, uint64_t window)
+READ_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
 
 class FileDesc(ctypes.Structure):
@@ -95,6 +115,9 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_index_buffer.argtypes = [vp, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
     L.sf_index_buffer_blocks.argtypes = [vp, u64, vp, vp, u64, ctypes.POINTER(BlockSig), vp]
     L.sf_index_file_blocks.argtypes = [ctypes.c_char_p, vp, vp, u64, ctypes.POINTER(BlockSig), vp]
+    L.sf_file_stamp_fd.argtypes = [i32, ctypes.POINTER(FileStamp)]
+    L.sf_index_fd_blocks.argtypes = [i32, ctypes.POINTER(FileStamp), vp, vp, u64, ctypes.POINTER(BlockSig), vp]
+    L.sf_index_fd_fixed.argtypes = [i32, ctypes.POINTER(FileStamp), u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
     L.sf_index_file.argtypes = [ctypes.c_char_p, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
     L.sf_index_file_range.argtypes = [ctypes.c_char_p, u64, u64, u32, ctypes.POINTER(BlockSig), u64, pu64]
     L.sf_index_fd.argtypes = [i32, u32, ctypes.POINTER(ctypes.POINTER(BlockSig)), pu64, vp]
@@ -112,6 +135,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_test_get_knob.argtypes = [ctypes.c_char_p, pi64]
     L.sf_test_get_stat.argtypes = [ctypes.c_char_p, pi64]
     L.sf_test_table_order.argtypes = [vp, u64, vp, vp]
+    L.sf_test_set_read_hook.argtypes = [READ_HOOK, vp]
     for name in EXPORTED + EXPORTED_TEST:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int
@@ -167,6 +191,23 @@ def get_stat(name: str) -> int:
     return v.value
 
 
+_read_hook_ref = None  # keeps the ctypes thunk alive while the library holds it
+
+
+def set_read_hook(fn) -> None:
+    """Test hook (sf_test_set_read_hook): fn(window) runs after each window a
+    pread route of the library has read, on the calling thread; None removes
+    it."""
+    global _read_hook_ref
+    if fn is None:
+        check(lib().sf_test_set_read_hook(READ_HOOK(), None), "sf_test_set_read_hook")
+        _read_hook_ref = None
+        return
+    thunk = READ_HOOK(lambda _arg, window: fn(int(window)))
+    check(lib().sf_test_set_read_hook(thunk, None), "sf_test_set_read_hook")
+    _read_hook_ref = thunk
+
+
 def _code_objects(path: str):
     """(triple, bytes) of every gfx950 code object in the library's
     .hip_fatbin section (one clang offload bundle per GPU translation unit)."""
@@ -202,7 +243,7 @@ def _code_objects(path: str):
 
 FIXED_KERNEL = "_ZN2sf17sha1_fixed_kernelILi128ELi1ELb0EEEvPKhmjmPhNS_11PadScheduleEPj"
 CHAINED_KERNEL = "_ZN2sf25sha1_fixed_chained_kernelILi128EEEvPKhmjmPhNS_11PadScheduleENS_8ChainJobES5_jjj"
-TABLE_KERNEL = "_ZN2sf17sha1_table_kernelILi128ELb0EEEvPKhmPKmPKjmPhPiPjS6_mm"
+TABLE_KERNEL = "_ZN2sf17sha1_table_kernelILi128ELb0EEEvPKhmPKmPKjmPhPiPjS6_S9_"
 
 
 def kernel_code_sha256(path: str = None, symbol: str = FIXED_KERNEL) -> str:

@@ -123,18 +123,21 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   return hip_err(hipGetLastError());
 }
 
-// CUs of the current device (cached).
+// CUs of the current device (cached per device: a process may drive GPUs or
+// partitions with different CU counts).
 inline unsigned device_cus() {
-  static std::atomic<int> cached{0};
-  int v = cached.load();
-  if (v > 0) return (unsigned)v;
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess ||
-      hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) {
+  static std::atomic<int> cached[kMaxDevices];
+  int d = 0, v = 0;
+  if (hipGetDevice(&d) != hipSuccess) {
     (void)hipGetLastError();
     return 64;  // conservative (a quarter of MI355X's CUs)
   }
-  cached.store(v);
+  if (d >= 0 && d < kMaxDevices && (v = cached[d].load(std::memory_order_relaxed)) > 0) return (unsigned)v;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) {
+    (void)hipGetLastError();
+    return 64;
+  }
+  if (d >= 0 && d < kMaxDevices) cached[d].store(v, std::memory_order_relaxed);
   return (unsigned)v;
 }
 
@@ -163,9 +166,12 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.
 // kernels, ~21 us for 0.5 M blocks, against ~56 us of GPU time for rocprim's
 // radix sort with its key kernel; profiles/r03/sort/); wider keys (the
 // SF_TABLE_CLASS_BITS A/B knob) keep rocprim.
+// *counter: a device word of the same workspace set to 0 on `s` (the
+// persistent table kernel's group counter).
 // Returns nullptr (unsorted launch) if anything fails.
-uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
+uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out, uint32_t** counter) {
   *ws_out = nullptr;
+  *counter = nullptr;
   // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
   const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
 
@@ -181,19 +187,21 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
 #define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
 #endif
   if (SF_CLASS_SORT && kbits == 8) {  // the default: one counting pass over 256 classes (sf_sort.hip)
-    const size_t ob = up(n * 4), total = ob + up(sfi::class_order_workspace(n));
+    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n)), total = ob + cb + 256;
     uint8_t* ws = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
     uint32_t* order = reinterpret_cast<uint32_t*>(ws);
-    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, s) != SF_OK) {
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + ob + cb);
+    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, ctr, s) != SF_OK) {
       (void)hipGetLastError();
       (void)hipFreeAsync(ws, s);
       return nullptr;
     }
     *ws_out = ws;
+    *counter = ctr;
     return order;
   }
   uint16_t *kin = nullptr, *kout = nullptr;
@@ -203,10 +211,16 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
     (void)hipGetLastError();
     return nullptr;
   }
-  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp);
+  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp) + 256;
   uint8_t* ws = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
     (void)hipGetLastError();
+    return nullptr;
+  }
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + 2 * kb + 2 * ib + up(tmp));
+  if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFreeAsync(ws, s);
     return nullptr;
   }
   kin = reinterpret_cast<uint16_t*>(ws);
@@ -223,6 +237,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
     return nullptr;
   }
   *ws_out = ws;
+  *counter = ctr;
   return iout;
 }
 
@@ -240,17 +255,17 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
     }
     return SF_OK;
   }
-  const unsigned grid = grid_for_blocks(nblocks);
+  unsigned grid = grid_for_blocks(nblocks);
   void* ws = nullptr;
-  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
-  // the critical-path test in sha1_table_kernel: a wave's length against
-  // the list's compressions (estimated) over the lanes of the device's
-  // resident waves (3 per SIMD)
-  const uint64_t work = len / 64 + nblocks;
-  const uint64_t lane_slots = 64ull * 4 * 3 * device_cus();
+  uint32_t* counter = nullptr;
+  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws, &counter) : nullptr;
+  // A sorted list: persistent waves claiming groups in the sort's order
+  // (sha1_table_kernel; the launcher in sf_table.hip starts at most the
+  // resident ones).
+  if (!order) counter = nullptr;
   const int rc = launch_table_kernel(weak != nullptr, grid, static_cast<const uint8_t*>(d_data), len, d_offsets,
-                                     d_sizes, nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order, work,
-                                     lane_slots, stream);
+                                     d_sizes, nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order,
+                                     counter, device_cus(), stream);
   if (ws) (void)hipFreeAsync(ws, stream);
   return rc;
 }
@@ -365,6 +380,7 @@ const char* sf_strerror(int code) {
   switch (code) {
     case SF_OK: return "ok";
     case SF_EIO: return "I/O error";
+    case SF_EAGAIN: return "the file changed while it was indexed (cut it again and retry)";
     case SF_ENOMEM: return "out of memory";
     case SF_ENODEV: return "no HIP device or HIP runtime error";
     case SF_EINVAL: return "invalid argument";
@@ -574,6 +590,18 @@ int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uin
 #ifndef SF_NO_CHAIN_HELPER
   if (total == 0) return launch_chain_helper(cj[0], cj[1], as_stream(stream));  // chains alone: helper waves
 #endif
+  // A chain wave of the block launch stages 64 files' runs through one
+  // buffer resource with 32-bit offsets (file b of the wave at b * run_len):
+  // runs of 62.9 MB or more (3.1 M blocks per file) could pass 4 GiB within
+  // one wave and wrap.  Such a job runs first, alone, on the helper-wave
+  // chain kernel (64-bit addressing), stream-ordered before this launch:
+  // its digests and states were completed by earlier launches.
+  for (int k = 0; k < 2; k++) {
+    if (!cj[k].waves || 64ull * cj[k].run_len + 128 <= 0xF0000000ull) continue;
+    const sf::ChainJob none = {};
+    if ((rc = launch_chain_helper(cj[k], none, as_stream(stream))) != SF_OK) return rc;
+    cj[k] = none;
+  }
   return launch_chained(static_cast<const uint8_t*>(d_data), total * (uint64_t)block_size, block_size, total,
                         static_cast<uint8_t*>(d_digests), pad_schedule(block_size), cj[0], cj[1], bwaves, wpf, wpp,
                         whole ? 0u : (uint32_t)(col_lo / 64), as_stream(stream));

@@ -648,6 +648,7 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
   const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
   const bool adv = fadvise_on();
   if (adv) (void)posix_fadvise(fd, (off_t)base, (off_t)len, POSIX_FADV_SEQUENTIAL);
+  uint64_t window = 0;
   auto fill = [&](uint8_t* dst, uint64_t off, uint64_t cap, uint64_t* nout, bool* eof) {
     const uint64_t n = std::min(cap, len - off);
     *nout = n;
@@ -673,6 +674,7 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
         if (r != SF_OK) rc.store(r);
       }
     });
+    read_hook(window++);
     return rc.load();
   };
   auto emit = [&](uint64_t first, uint64_t nb, const uint8_t* dg, uint64_t bytes) {
@@ -856,6 +858,105 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
   return rc;
 }
 
+// ------------------------------------------------ one open regular file
+// index_file opens the file once and takes its mtime, its boundaries and its
+// bytes from that one handle (src/index.rs:615-625).  The descriptor routes
+// read the caller's open file with pread and compare its stamp (fstat) when
+// the call starts -- against the caller's, taken before its chunker read the
+// file -- and after the last window is read: a file changed in between gives
+// SF_EAGAIN, never rows that mix one version's boundaries with another's bytes.
+bool stamp_of(int fd, sf_file_stamp* s, mode_t* mode) {
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) return false;
+  s->dev = (uint64_t)sb.st_dev;
+  s->ino = (uint64_t)sb.st_ino;
+  s->size = (uint64_t)sb.st_size;
+  s->nlink = (uint64_t)sb.st_nlink;
+  s->mtime_sec = (int64_t)sb.st_mtim.tv_sec;
+  s->mtime_nsec = (int64_t)sb.st_mtim.tv_nsec;
+  s->ctime_sec = (int64_t)sb.st_ctim.tv_sec;
+  s->ctime_nsec = (int64_t)sb.st_ctim.tv_nsec;
+  if (mode) *mode = sb.st_mode;
+  return true;
+}
+
+// ctime also moves when a link is added or removed (a rename over the path
+// unlinks the open file, whose bytes do not change): it is compared only
+// while the link count stays the same (include/syncfast_amd.h).
+bool same_stamp(const sf_file_stamp& a, const sf_file_stamp& b) {
+  return a.dev == b.dev && a.ino == b.ino && a.size == b.size && a.mtime_sec == b.mtime_sec &&
+         a.mtime_nsec == b.mtime_nsec &&
+         (a.nlink != b.nlink || (a.ctime_sec == b.ctime_sec && a.ctime_nsec == b.ctime_nsec));
+}
+
+// body(stamp, mode) between two stamps of fd.  A read that came up short (the
+// file shrank: SF_EIO) or a complete one over a file whose stamp moved is
+// SF_EAGAIN; other results (argument errors, SF_ENOSPC, device errors) pass.
+template <typename Body>
+int stamped(int fd, const sf_file_stamp* expect, Body body) {
+  sf_file_stamp before{}, after{};
+  mode_t mode = 0;
+  if (!stamp_of(fd, &before, &mode)) return SF_EIO;
+  if (expect && !same_stamp(before, *expect)) return SF_EAGAIN;
+  const int rc = body(before, mode);
+  if (rc != SF_OK && rc != SF_EIO) return rc;
+  if (!stamp_of(fd, &after, nullptr)) return SF_EIO;
+  return same_stamp(before, after) ? rc : SF_EAGAIN;
+}
+
+// Bytes [w0, w0 + m) of fd into dst: pread slices on the reader threads.  A
+// short read (the file shrank after the list was made) is SF_EIO.
+int pread_window(int fd, uint8_t* dst, uint64_t w0, uint64_t m) {
+  const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
+  const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(m, nthreads));
+  const uint64_t nslices = ceil_div(m, slice);
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> frc{SF_OK};
+  run_pool((unsigned)std::min<uint64_t>(nthreads, std::max<uint64_t>(nslices, 1)), [&] {
+    for (uint64_t k; (k = next.fetch_add(1)) < nslices && frc.load() == SF_OK;) {
+      const uint64_t a = k * slice, e = std::min(m, a + slice);
+      for (uint64_t got = a; got < e;) {
+        const ssize_t r = pread(fd, dst + got, e - got, (off_t)(w0 + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          frc.store(SF_EIO);
+          break;
+        }
+        got += (uint64_t)r;
+      }
+    }
+  });
+  return frc.load();
+}
+
+void empty_blocks_hash(uint8_t* blocks_hash) {  // compute_blocks_hash of no blocks: SHA-1("")
+  if (!blocks_hash) return;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  sf_host_sha1_final(&bh, blocks_hash);
+}
+
+// An explicit list over the regular file open on fd, len bytes long: checked
+// against len, then windows pread into the pinned stages of the list pipeline.
+int index_fd_list(int fd, uint64_t len, const uint64_t* offsets, const uint32_t* sizes, uint64_t n,
+                  sf_block_sig* out, uint8_t* blocks_hash) {
+  for (uint64_t i = 0; i < n; i++) {
+    if (offsets[i] > len || sizes[i] > len - offsets[i]) return SF_ERANGE;
+    if (i && offsets[i] < offsets[i - 1]) return SF_EINVAL;
+  }
+  if (n == 0) {
+    empty_blocks_hash(blocks_hash);
+    return SF_OK;
+  }
+  uint64_t window = 0;
+  auto fill = [&](uint8_t* dst, uint64_t w0, uint64_t w1) {
+    const int r = pread_window(fd, dst, w0, w1 - w0);
+    read_hook(window++);
+    return r;
+  };
+  return index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash);
+}
+
 }  // namespace
 
 extern "C" {
@@ -894,46 +995,44 @@ static int sf_index_file_blocks_body(const char* path, const uint64_t* offsets, 
   } f{open(path, O_RDONLY | O_NONBLOCK)};  // a FIFO is refused below, not waited on
   const int fd = f.fd;
   if (fd < 0) return SF_EIO;
-  struct stat sb;
-  if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) return SF_EIO;  // the list names file offsets: a seekable file
-  const uint64_t len = (uint64_t)sb.st_size;
-  for (uint64_t i = 0; i < n; i++) {
-    if (offsets[i] > len || sizes[i] > len - offsets[i]) return SF_ERANGE;
-    if (i && offsets[i] < offsets[i - 1]) return SF_EINVAL;
-  }
-  int rc = SF_OK;
-  if (n == 0) {
-    if (blocks_hash) {
-      sf_host_sha1_stream bh;
-      sf_host_sha1_begin(&bh);
-      sf_host_sha1_final(&bh, blocks_hash);
+  return stamped(fd, nullptr, [&](const sf_file_stamp& st, mode_t mode) {
+    if (!S_ISREG(mode)) return SF_EIO;  // the list names file offsets: a seekable file
+    return index_fd_list(fd, st.size, offsets, sizes, n, out, blocks_hash);
+  });
+}
+
+static int sf_index_fd_blocks_body(int fd, const sf_file_stamp* expect, const uint64_t* offsets,
+                                   const uint32_t* sizes, uint64_t n, sf_block_sig* out, uint8_t* blocks_hash) {
+  if (fd < 0 || (n && (!offsets || !sizes || !out))) return SF_EINVAL;
+  return stamped(fd, expect, [&](const sf_file_stamp& st, mode_t mode) {
+    if (!S_ISREG(mode)) return SF_EINVAL;  // a pipe cannot be read twice: sf_index_buffer_blocks
+    return index_fd_list(fd, st.size, offsets, sizes, n, out, blocks_hash);
+  });
+}
+
+static int sf_index_fd_fixed_body(int fd, const sf_file_stamp* expect, uint32_t block_size, sf_block_sig* out,
+                                  uint64_t cap, uint64_t* n_out, uint8_t* blocks_hash) {
+  if (n_out) *n_out = 0;
+  int rc = check_fixed_args(0, block_size);
+  if (rc) return rc;
+  if (fd < 0) return SF_EINVAL;
+  return stamped(fd, expect, [&](const sf_file_stamp& st, mode_t mode) {
+    if (!S_ISREG(mode)) return SF_EINVAL;  // a stream: sf_index_fd
+    const uint64_t nb = st.size ? ceil_div(st.size, block_size) : 0;
+    if (n_out) *n_out = nb;
+    if (nb > cap) return SF_ENOSPC;
+    if (nb && !out) return SF_EINVAL;
+    if (nb == 0) {
+      empty_blocks_hash(blocks_hash);
+      return SF_OK;
     }
-  } else {
-    const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
-    // windows are read with pread slices on the reader threads; a short read
-    // (the file shrank after the list was made) is SF_EIO
-    auto fill = [&](uint8_t* dst, uint64_t w0, uint64_t w1) {
-      const uint64_t m = w1 - w0;
-      const uint64_t slice = std::max<uint64_t>(4ull << 20, ceil_div(m, nthreads));
-      const uint64_t nslices = ceil_div(m, slice);
-      std::atomic<uint64_t> next{0};
-      std::atomic<int> frc{SF_OK};
-      run_pool((unsigned)std::min<uint64_t>(nthreads, std::max<uint64_t>(nslices, 1)), [&] {
-        for (uint64_t k; (k = next.fetch_add(1)) < nslices && frc.load() == SF_OK;) {
-          const uint64_t a = k * slice, e = std::min(m, a + slice);
-          for (uint64_t got = a; got < e;) {
-            const ssize_t r = pread(fd, dst + got, e - got, (off_t)(w0 + got));
-            if (r < 0 && errno == EINTR) continue;
-            if (r <= 0) { frc.store(SF_EIO); break; }
-            got += (uint64_t)r;
-          }
-        }
-      });
-      return frc.load();
-    };
-    rc = index_list_pipeline(fill, offsets, sizes, n, out, blocks_hash);
-  }
-  return rc;
+    return index_file_pread(fd, 0, st.size, block_size, out, blocks_hash);
+  });
+}
+
+int sf_file_stamp_fd(int fd, sf_file_stamp* out) {
+  if (fd < 0 || !out) return SF_EINVAL;
+  return stamp_of(fd, out, nullptr) ? SF_OK : SF_EIO;
 }
 
 static int sf_index_buffer_body(const uint8_t* data, uint64_t len, uint32_t block_size, sf_block_sig* out, uint64_t cap,
@@ -1110,6 +1209,16 @@ int sf_index_buffer_blocks(const uint8_t* data, uint64_t len, const uint64_t* of
 int sf_index_file_blocks(const char* path, const uint64_t* offsets, const uint32_t* sizes, uint64_t n_blocks,
                          sf_block_sig* out, uint8_t blocks_hash[20]) {
   return guarded([&] { return sf_index_file_blocks_body(path, offsets, sizes, n_blocks, out, blocks_hash); });
+}
+
+int sf_index_fd_blocks(int fd, const sf_file_stamp* expect, const uint64_t* offsets, const uint32_t* sizes,
+                       uint64_t n_blocks, sf_block_sig* out, uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_fd_blocks_body(fd, expect, offsets, sizes, n_blocks, out, blocks_hash); });
+}
+
+int sf_index_fd_fixed(int fd, const sf_file_stamp* expect, uint32_t block_size, sf_block_sig* out, uint64_t cap,
+                      uint64_t* n_out, uint8_t blocks_hash[20]) {
+  return guarded([&] { return sf_index_fd_fixed_body(fd, expect, block_size, out, cap, n_out, blocks_hash); });
 }
 
 int sf_index_file(const char* path, uint32_t block_size, sf_block_sig* out, uint64_t cap, uint64_t* n_out,

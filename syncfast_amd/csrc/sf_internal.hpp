@@ -61,6 +61,10 @@ enum Stat { S_PAGES_LOCKED, S_NOT_ANON_REFUSED, S_COUNT };
 extern std::atomic<int64_t> g_stat[S_COUNT];
 inline void stat_add(Stat s, int64_t v = 1) { g_stat[s].fetch_add(v, std::memory_order_relaxed); }
 
+// Test hook (sf_test_set_read_hook, sf_knobs.cpp): the pread routes call it
+// after each window of a regular file has been read.
+void read_hook(uint64_t window);
+
 // A C++ exception must not cross the extern "C" boundary: a C or Rust caller
 // would get std::terminate.  Every entry point that allocates, starts threads
 // or takes locks on the host runs its body through guarded(): host allocation
@@ -267,12 +271,17 @@ inline unsigned io_threads() {
 // bytes of device memory.  Stream-ordered on s.
 size_t class_order_workspace(uint64_t n);
 // sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
-// translation unit); SF_OK or the launch error.
+// translation unit); SF_OK or the launch error.  next_group: NULL (grid
+// workgroups, one group of 64 blocks per wave) or a zeroed device counter
+// (persistent waves that claim groups in order: at most the waves `cus` CUs
+// hold at once are started).
 int launch_table_kernel(bool weak_form, unsigned grid, const uint8_t* d_data, uint64_t len,
                         const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests,
-                        int* d_status, uint32_t* weak, const uint32_t* order, uint64_t work, uint64_t lane_slots,
+                        int* d_status, uint32_t* weak, const uint32_t* order, uint32_t* next_group, unsigned cus,
                         hipStream_t stream);
+// zero_word (may be NULL): a device word the sort sets to 0, stream-ordered
+// (the persistent table kernel's group counter).
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
-                hipStream_t s);
+                uint32_t* zero_word, hipStream_t s);
 
 }  // namespace sfi

@@ -360,12 +360,26 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     return;
   }
   // Remaining data chunks and the padding chunk(s), per lane.
-  const uint32_t nch = n_chunks(size);
-  for (uint32_t c = c_done; c < geo.max_nch; ++c) {
-    if (valid && c < nch) {
-      uint32_t w[16];
-      build_tail_chunk(w, data + off, size, c, nch);
-      st.compress(w);
+  if constexpr (HAS_PAD) {
+    const uint32_t nch = n_chunks(size);
+    for (uint32_t c = c_done; c < geo.max_nch; ++c) {
+      if (valid && c < nch) {
+        uint32_t w[16];
+        build_tail_chunk(w, data + off, size, c, nch);
+        st.compress(w);
+      }
+    }
+  } else {
+    // An explicit list's block may be any uint32 size: the index of its last
+    // chunk, (size + 8) / 64, without the 32-bit wrap of n_chunks from
+    // 2^32 - 8.
+    const uint32_t last = (size >> 6) + ((size & 63u) >= 56u ? 1u : 0u);
+    for (uint32_t c = c_done; c < geo.max_nch; ++c) {
+      if (valid && c <= last) {
+        uint32_t w[16];
+        build_tail_chunk(w, data + off, size, c, last + 1u);
+        st.compress(w);
+      }
     }
   }
 }
@@ -798,7 +812,10 @@ __device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t s
 // big-endian) are in w: keep the rem = size - 64c data bytes, then the 0x80
 // byte, zeros, and the bit length if c is the last chunk (nch - 1).
 __device__ __forceinline__ void finish_chunk(uint32_t (&w)[16], uint32_t size, uint32_t c, uint32_t nch) {
-  const int rem = (int)size - (int)(c * 64u);
+  // size < 0xF0000000 on the slot path, so c * 64 does not wrap; the
+  // difference is taken in uint32 and then read as signed: a padding-only
+  // chunk (c * 64 > size) gives a small negative rem for sizes >= 2^31 too
+  const int rem = (int)(size - c * 64u);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int v = rem - 4 * j;  // data bytes in word j
@@ -841,7 +858,9 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
                                                Sha1& st) {
   const int lane = threadIdx.x & 63;
   st.init();
-  const uint32_t nch = n_chunks(size);                 // compressions of this lane's message
+  // compressions of this lane's message (the slot path's blocks are < 3.75
+  // GiB, so the 32-bit form cannot wrap; the wide form cost 5 spilled VGPRs)
+  const uint32_t nch = n_chunks(size);
   const uint32_t mine = valid ? size / 64u : 0u;       // its whole data chunks
   const uint32_t nsteps = wave_max_u32(valid ? (nch + 1u) / 2u : 0u);
   const uint32_t rel = valid ? (uint32_t)((off & ~3ull) - base) : 0u;  // pieces start at the block's dword
@@ -896,42 +915,32 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
   }
 }
 
+#ifndef SF_TABLE_LB
+#define SF_TABLE_LB 3  // waves/SIMD the register budget is sized for (A/B: make tablevariant TEXTRA=-DSF_TABLE_LB=2)
+#endif
+#ifndef SF_TABLE_WG
+#define SF_TABLE_WG 4  // waves per workgroup (A/B: 1, 2)
+#endif
+#ifndef SF_TABLE_PERSIST
+#define SF_TABLE_PERSIST 0  // 1: persistent waves claiming groups (A/B record, slower)
+#endif
+
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
 // Used for content-defined boundaries, the reference KAT boundaries, ragged
 // many-file batches, and (over the digest table) per-file blocks_hash.
 // A block outside [0, len) is not read: its digest is zeroed and *status is
 // set to -34 (SF_ERANGE).
-// `order` (optional): the blocks in the order the waves take them -- wave w
-// hashes blocks order[64w .. 64w+63] and writes each digest at the block's
-// own index.  The launcher passes the blocks sorted by compression count,
-// largest first: a wave runs as long as its longest block, so a list of
-// mixed sizes (content-defined blocks, files' short last blocks) wastes
-// most lanes unless each wave's 64 blocks are about the same length; and
-// handing out the longest blocks first keeps the grid's tail short (LPT).
-// Critical-path priority (`work`, with `order`; round 3).  The longest
-// waves start first, but at a third of their SIMD's issue they could still
-// be running after every short wave is done.  A wave whose length exceeds
-// the list's average work per wave slot (work / lane_slots, in
-// compressions) issues at priority 2, so the short waves beside it fill the
-// cycles its dependency stalls leave.  `work` is the launcher's estimate
-// len / 64 + nblocks (exact for a list that tiles the data once).  Measured
-// (profiles/r03/cdc_prio/): this machine code runs the CDC-like 4 GiB list
-// at 2991 GiB/s, the same code with priority 0 at 2954, builds without the
-// test at 2887 -- most of the gain is this compiled form, so its machine
-// code is pinned (table_kernel.json, a CPU test); re-expressions of the
-// same test compiled to slower code.
-template <int TILE, bool WEAK = false>
-__global__ void __launch_bounds__(kThreads, 3)  // 3 waves/SIMD, as the fixed kernel (the weak form asked 169 VGPRs)
-sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
-                  const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
-                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
-                  uint64_t work, uint64_t lane_slots) {
-  constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
-  __shared__ uint4 smem[kWavesPerWG * kWaveTile];
+// Group g of the list = 64 blocks, one lane each: order[64g .. 64g + 63] when
+// the launcher sorted the list (each digest is written at the block's own
+// index), else blocks 64g .. 64g + 63.
+template <int TILE, bool WEAK>
+__device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, uint64_t len,
+                                            const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ sizes,
+                                            uint64_t nblocks, uint8_t* __restrict__ digests, int* __restrict__ status,
+                                            uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
+                                            uint64_t g, uint4* __restrict__ tile) {
   const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 64;
-  if (first >= nblocks) return;
+  const uint64_t first = g * 64;
   bool valid = first + lane < nblocks;
   const uint64_t blk = (order && valid) ? (uint64_t)order[first + lane] : first + lane;
   uint64_t off = 0;
@@ -953,7 +962,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   geo.span = hi - lo;
   geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
   geo.max_size = wave_max_u32(valid ? size : 0u);
-  geo.max_nch = wave_max_u32(valid ? n_chunks(size) : 0u);
+  geo.max_nch = wave_max_u32(valid ? n_chunks_wide(size) : 0u);
   const bool aligned = !valid || ((off & 15u) == 0);
   geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
                ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
@@ -961,12 +970,25 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 #ifndef SF_TABLE_PRIO
 #define SF_TABLE_PRIO 1  // 0: no critical-path priority (A/B)
 #endif
-  if (SF_TABLE_PRIO && order && work && (uint64_t)geo.max_nch * lane_slots >= work)
-    __builtin_amdgcn_s_setprio(2);
+#if SF_TABLE_PRIO && !SF_TABLE_PERSIST
+  // Critical-path priority (round 3): a sorted group longer than the list's
+  // compressions per lane of 3 waves on 1024 SIMDs (len / 64 + nblocks: exact
+  // for a list that tiles the data once) issues at priority 2.
+  if (order && (uint64_t)geo.max_nch * (64ull * 3 * 1024) >= len / 64 + nblocks) __builtin_amdgcn_s_setprio(2);
+#endif
+#ifdef SF_WAVE_TRACE
+  // Diagnostic build only (make tablevariant TEXTRA=-DSF_WAVE_TRACE): each
+  // group's start / end (s_memrealtime, 100 MHz), where it ran (HW_ID,
+  // XCC_ID) and its length, into the trace buffer passed as `weak` (unused
+  // by the plain kernel); scripts/table_trace.py reads it.
+  uint64_t trace_t0 = 0;
+  if constexpr (!WEAK) {
+    if (weak) trace_t0 = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 
   Sha1 st;
   Adler wk;
-  uint4* tile = smem + wid * kWaveTile;
 #ifndef SF_LIST_ALIGNED_TOO
 #define SF_LIST_ALIGNED_TOO 0  // 1: every 16-B aligned wave takes the 144-B slot path too (A/B)
 #endif
@@ -993,11 +1015,97 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
       if constexpr (WEAK) weak[blk] = wk.fin();
     }
   }
+#ifdef SF_WAVE_TRACE
+  if constexpr (!WEAK) {
+    if (weak) {
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID, 32 bits
+      const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID, 4 bits
+      const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+      if (lane == 0) {
+        uint32_t* t = weak + g * 8;
+        t[0] = (uint32_t)trace_t0;
+        t[1] = (uint32_t)(trace_t0 >> 32);
+        t[2] = (uint32_t)t1;
+        t[3] = (uint32_t)(t1 >> 32);
+        t[4] = hwid;
+        t[5] = xcc;
+        t[6] = geo.max_nch;
+        t[7] = (list_path ? 1u : 0u) | (nvalid << 8);
+      }
+    }
+  }
+#endif
 }
 
-// Sort keys of an explicit block list for sha1_table_kernel's `order`: the
-// block's compression count on a log scale with `mbits` mantissa bits (the
-// launcher's default 6: classes <= 1.6 % wide, exact below 64), and its index.  A class holds many blocks, so
+// The explicit-list kernel: wave w of the grid hashes group w (one group of
+// 64 blocks per wave, SF_TABLE_WG waves per workgroup).  How the waves of a
+// sorted list are scheduled decides its rate (DESIGN.md section 3.4, round
+// 4; scripts/table_trace.py records every wave's start, end and SIMD):
+//   * the sequencer issues the OLDEST wave of a SIMD first, so a wave that
+//     starts first -- with the sort, one of the longest groups -- runs at
+//     nearly the rate it would alone (1.33 us per compression beside two
+//     other waves, the 4 KiB list's waves 2.9 us), and the younger waves
+//     fill its gaps: hardware dispatch in the sort's order already gives the
+//     longest groups the critical path;
+//   * persistent waves that claim groups from a counter (SF_TABLE_PERSIST=1,
+//     kept for the record) lose that: a wave's age is its launch, not its
+//     group's, so an old wave that keeps claiming groups starves a younger
+//     neighbour, whose group then ends last (2501 vs 3031 GiB/s);
+//   * what is left is the end of the launch: a SIMD idles once its last
+//     waves are done, and with four-wave workgroups a slot is handed out
+//     again only when all four are (SF_TABLE_WG).
+// next_group (SF_TABLE_PERSIST=1 builds only): the claim counter.
+template <int TILE, bool WEAK = false>
+__global__ void __launch_bounds__(64 * SF_TABLE_WG, SF_TABLE_LB)
+sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
+                  const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
+                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
+                  uint32_t* __restrict__ next_group) {
+  constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
+  __shared__ uint4 smem[SF_TABLE_WG * kWaveTile];
+  const int wid = SF_TABLE_WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint4* tile = smem + wid * kWaveTile;
+  const uint32_t ngroups = (uint32_t)((nblocks + 63) / 64);  // <= 2^25: the launcher splits at 2^31 blocks
+#if SF_TABLE_PERSIST
+  // every claim moves the counter on, so each wave exits once it passes ngroups
+  auto claim = [&]() -> uint32_t {
+    uint32_t k = 0;
+    if ((threadIdx.x & 63) == 0) k = __hip_atomic_fetch_add(next_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(k);
+  };
+  uint32_t g = next_group ? claim() : blockIdx.x * SF_TABLE_WG + wid;
+  const uint32_t launched = gridDim.x * SF_TABLE_WG;
+  while (g < ngroups) {  // one call site: the group body is inlined once
+#if SF_TABLE_PERSIST == 2
+    // groups issue in claim order, not in their waves' launch order: the
+    // claim's generation (g / waves launched) sets the wave's priority
+    const uint32_t gen = g / launched;
+    if (gen == 0) __builtin_amdgcn_s_setprio(3);
+    else if (gen == 1) __builtin_amdgcn_s_setprio(2);
+    else if (gen == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)launched;
+#endif
+    table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
+    if (!next_group) break;
+    g = claim();
+  }
+#else
+  (void)next_group;
+  const uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
+  if (g < ngroups) table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
+#endif
+}
+
+// Sort keys of an explicit block list for sha1_table_kernel's `order` (the
+// rocprim form, kept for the wider keys of the SF_TABLE_CLASS_BITS A/B knob;
+// the default 4 mantissa bits take the counting sort of sf_sort.hip): the
+// block's compression count on a log scale with `mbits` mantissa bits
+// (classes 6.25 % wide with 4 bits, exact below 16; the key is clamped to
+// kmax = 255, so every block of >= 2^16 compressions shares the top class),
+// and its index.  A class holds many blocks, so
 // a wave's 64 blocks (consecutive in the stable sort: list order within a
 // class) lie close together in memory; an exact-count key spreads them over
 // the whole buffer (every nch value is rare), and 64 lanes streaming from 64
@@ -1017,7 +1125,7 @@ table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __re
                   uint32_t* __restrict__ idx, uint32_t mbits, uint32_t kmax) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t k = length_class(n_chunks(sizes[i]), mbits);
+  const uint32_t k = length_class(n_chunks_wide(sizes[i]), mbits);
   keys[i] = (uint16_t)(k < kmax ? k : kmax);
   idx[i] = (uint32_t)i;
 }

@@ -36,6 +36,16 @@ const KnobDef kKnobDefs[K_COUNT] = {
 
 std::atomic<int64_t> g_knob[K_COUNT];
 std::atomic<int64_t> g_stat[S_COUNT];
+
+namespace {
+std::atomic<sf_test_read_hook_fn> g_read_hook{nullptr};
+std::atomic<void*> g_read_hook_arg{nullptr};
+}  // namespace
+
+void read_hook(uint64_t window) {
+  const sf_test_read_hook_fn fn = g_read_hook.load(std::memory_order_acquire);
+  if (fn) fn(g_read_hook_arg.load(std::memory_order_relaxed), window);
+}
 static const char* const kStatNames[S_COUNT] = {"pages_locked", "not_anon_refused"};
 
 namespace {
@@ -74,6 +84,12 @@ int sf_test_get_stat(const char* name, int64_t* value) {
       return SF_OK;
     }
   return SF_EINVAL;
+}
+
+int sf_test_set_read_hook(sf_test_read_hook_fn fn, void* arg) {
+  g_read_hook_arg.store(arg, std::memory_order_relaxed);
+  g_read_hook.store(fn, std::memory_order_release);
+  return SF_OK;
 }
 
 int sf_test_get_knob(const char* name, int64_t* value) {

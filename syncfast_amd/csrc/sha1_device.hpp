@@ -177,8 +177,16 @@ __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
   return v;
 }
 
-// Number of SHA-1 compressions for a message of `size` bytes.
+// Number of SHA-1 compressions for a message of `size` bytes.  (size + 8)
+// wraps for size >= 2^32 - 8: the fixed tiling's blocks (<= 32 MiB) and the
+// digest runs (< 2^32 - 16) use this form; explicit lists, whose sizes are
+// any uint32, use n_chunks_wide.
 __device__ __forceinline__ uint32_t n_chunks(uint32_t size) { return (size + 8u) / 64u + 1u; }
+// The same count for any uint32 size: (size + 8) / 64 + 1 without the
+// 32-bit wrap (2^26 + 1 for size = 2^32 - 1).
+__device__ __forceinline__ uint32_t n_chunks_wide(uint32_t size) {
+  return (size >> 6) + 1u + (((size & 63u) + 8u) >> 6);
+}
 
 // Chunk c (0-based) of the padded message of a block of `size` bytes that
 // starts at p (global memory).  Reads only bytes [0, size) of the block.

@@ -14,7 +14,7 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
-from ._lib import SF_EINVAL, SF_EIO, SF_ENOSPC, BlockSig, check, lib
+from ._lib import SF_EINVAL, SF_EIO, SF_ENOSPC, BlockSig, FileStamp, check, lib
 
 SIG_DTYPE = np.dtype([("offset", "<u8"), ("size", "<u4"), ("sha1", "u1", (20,))], align=True)
 assert SIG_DTYPE.itemsize == ctypes.sizeof(BlockSig) == 32
@@ -75,6 +75,48 @@ def index_file_blocks(path, offsets, sizes) -> Tuple[np.ndarray, bytes]:
                                      out.ctypes.data_as(ctypes.POINTER(BlockSig)), bh),
           f"sf_index_file_blocks({os.fsdecode(path)})")
     return out[:n], bytes(bh)
+
+
+def file_stamp(fd: int) -> FileStamp:
+    """sf_file_stamp_fd: fstat's identity of the file open on fd (dev, ino,
+    size, mtime, ctime), taken before a chunker reads it."""
+    st = FileStamp()
+    check(lib().sf_file_stamp_fd(int(fd), ctypes.byref(st)), "sf_file_stamp_fd")
+    return st
+
+
+def index_fd_blocks(fd: int, offsets, sizes, stamp: FileStamp = None) -> Tuple[np.ndarray, bytes]:
+    """An explicit list over the regular file OPEN on fd (sf_index_fd_blocks):
+    the chunker's own handle, read again with pread, so the bytes hashed are
+    the file the chunker cut even if another file was renamed over its path.
+    `stamp` (file_stamp before chunking): SfError SF_EAGAIN if the file
+    differs from it at the call or changes before the last window is read."""
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
+    szs = np.ascontiguousarray(sizes, dtype=np.uint32).reshape(-1)
+    if offs.size != szs.size:
+        raise ValueError("offsets and sizes differ in length")
+    n = offs.size
+    out = np.zeros(max(n, 1), SIG_DTYPE)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_fd_blocks(int(fd), ctypes.byref(stamp) if stamp is not None else None,
+                                   offs.ctypes.data if n else None, szs.ctypes.data if n else None, n,
+                                   out.ctypes.data_as(ctypes.POINTER(BlockSig)), bh),
+          "sf_index_fd_blocks")
+    return out[:n], bytes(bh)
+
+
+def index_fd_fixed(fd: int, block_size: int, stamp: FileStamp = None) -> Tuple[np.ndarray, bytes]:
+    """Fixed tiling of the regular file open on fd (sf_index_fd_fixed), with
+    the same stamp checks as index_fd_blocks."""
+    size = os.fstat(int(fd)).st_size
+    n = (size + block_size - 1) // block_size if size else 0
+    out = np.zeros(max(n, 1), SIG_DTYPE)
+    nout = ctypes.c_uint64(0)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_fd_fixed(int(fd), ctypes.byref(stamp) if stamp is not None else None, block_size,
+                                  out.ctypes.data_as(ctypes.POINTER(BlockSig)), n, ctypes.byref(nout), bh),
+          "sf_index_fd_fixed")
+    return out[:nout.value], bytes(bh)
 
 
 def release_cache() -> None:

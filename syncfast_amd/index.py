@@ -19,7 +19,7 @@ caller chose when opening the index:
     blocks are the reference's by construction; every block's SHA-1 and the
     ``blocks_hash`` come from the GPU.  ``stream=True`` hands ``fn`` the open
     file (as ``chunker.stream(file)`` reads it) and the library re-reads the
-    file by windows (sf_index_file_blocks), so no file is held whole;
+    same open file by windows (sf_index_fd_blocks), so no file is held whole;
   * ``FixedChunker(block_size)`` -- fixed tiling, the BASELINE configs' mode.
     NOT the reference's default blocks: an index built this way only works
     with peers that use the same mode and read a block as its row's
@@ -59,10 +59,15 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import host
+from ._lib import SF_EAGAIN, SfError, same_stamp
 from .digest import HashDigest
 from .timestamp import DateTimeUtc
 
 log = logging.getLogger("syncfast_amd.index")
+
+# index_file: times a file that keeps changing while it is indexed
+# (SF_EAGAIN from the descriptor routes) is opened and indexed again.
+CHANGED_RETRIES = 3
 
 SCHEMA = """
     CREATE TABLE files(
@@ -131,6 +136,11 @@ def _mtime(f) -> DateTimeUtc:
     return DateTimeUtc.from_ns(os.fstat(f.fileno()).st_mtime_ns)
 
 
+def _stamp_moved(fd: int, stamp) -> bool:
+    """Has the file open on fd changed since `stamp` (host.file_stamp)?"""
+    return not same_stamp(host.file_stamp(fd), stamp)
+
+
 def _now() -> DateTimeUtc:
     """``chrono::Utc::now()`` (src/index.rs:265)."""
     import time
@@ -166,7 +176,7 @@ class BoundaryChunker:
     len(data)); with ``stream=True``, fn(file) reads an open binary file to
     its end (as ``chunker.stream(file)`` does, src/index.rs:625) and returns
     the sizes, and the file is re-read by windows on the library side
-    (sf_index_file_blocks) instead of being held whole.  The signatures are
+    (sf_index_fd_blocks) instead of being held whole.  The signatures are
     computed by the GPU kernel (explicit-block-list entry points)."""
 
     def __init__(self, fn: Callable, stream: bool = False):
@@ -455,27 +465,53 @@ class Index:
         the digests in offset order, which is the order the rows are inserted
         in and so the order compute_blocks_hash's SELECT reads them back in
         (src/index.rs:661-682) -- the same value without re-reading the rows.
-        BoundaryChunker(stream=True) on a regular file: the chunker streams
-        the open file and the library re-reads it by windows
-        (sf_index_file_blocks); FixedChunker: sf_index_file / sf_index_fd;
-        a BoundaryChunker over bytes: the file's bytes and the list go to
-        sf_index_buffer_blocks."""
+        Like the reference (src/index.rs:615-625), ONE open of the file gives
+        the mtime, the boundaries and the bytes: BoundaryChunker(stream=True)
+        on a regular file streams the open file and the library re-reads that
+        same descriptor by windows (sf_index_fd_blocks); FixedChunker:
+        sf_index_fd_fixed on it (sf_index_fd for a FIFO); a BoundaryChunker
+        over bytes: the file's bytes and the list go to
+        sf_index_buffer_blocks.  The descriptor routes compare the file's
+        stamp (fstat, taken before the chunker read it) when they start and
+        after their last read: a file written while it is indexed is indexed
+        again from a new open (at most CHANGED_RETRIES times, then the
+        SF_EAGAIN error propagates), never stored as rows that mix two
+        versions of it."""
         self._need_chunker()
+        for attempt in range(CHANGED_RETRIES):
+            try:
+                self._index_file_once(path, name, force=attempt > 0)
+                return
+            except SfError as e:
+                if e.code != SF_EAGAIN or attempt + 1 == CHANGED_RETRIES:
+                    raise
+                log.info("File %s changed while it was indexed, indexing it again", path)
+
+    def _index_file_once(self, path, name, force: bool) -> None:
         ch = self.chunker
         native = None  # (rows, blocks_hash) from a native route
         with open(path, "rb") as f:  # File::open first: same error on a missing file
-            file_id, up_to_date = self.add_file(name, _mtime(f))
+            seekable = _seekable(f)
+            stamp = host.file_stamp(f.fileno()) if seekable and (isinstance(ch, FixedChunker) or ch.stream) else None
+            mtime = DateTimeUtc.from_ns(stamp.mtime_sec * 10**9 + stamp.mtime_nsec) if stamp else _mtime(f)
+            file_id, up_to_date = self.add_file(name, mtime)
             if up_to_date:
-                return
+                if not force:
+                    return
+                # a retry after SF_EAGAIN whose mtime did not move (the writer
+                # restored it, or only the ctime changed): index it anyway
+                self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
             if isinstance(ch, FixedChunker):
-                if _seekable(f):
-                    native = host.index_file(path, ch.block_size)
+                if seekable:
+                    native = host.index_fd_fixed(f.fileno(), ch.block_size, stamp)
                 else:  # a FIFO: read sequentially from this open, as File::open + read do
                     native = host.index_fd(f.fileno(), ch.block_size)
-            elif ch.stream and _seekable(f):
-                size = os.fstat(f.fileno()).st_size
-                sizes = _sizes_ok(ch.fn(f), size)
-                native = host.index_file_blocks(path, _offsets(sizes), np.asarray(sizes, np.uint32))
+            elif ch.stream and seekable:
+                sizes = [int(x) for x in ch.fn(f)]
+                if sum(sizes) != stamp.size and _stamp_moved(f.fileno(), stamp):
+                    raise SfError(SF_EAGAIN, f"index_file({os.fsdecode(path)})")  # written while chunked
+                sizes = _sizes_ok(sizes, stamp.size)
+                native = host.index_fd_blocks(f.fileno(), _offsets(sizes), np.asarray(sizes, np.uint32), stamp)
             else:
                 rows = signatures_of_bytes(f.read(), ch)
         if native is not None:

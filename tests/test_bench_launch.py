@@ -59,6 +59,24 @@ def test_multi_block_three_ranks():
     assert m["steps_as_root"] == [2, 2, 2]
 
 
+def test_config4_multi_line_names_its_workload():
+    """The driver's 8-GPU config-4 run must not mislabel itself: an N > 1
+    config-4 line carries the `multi` block and config 4's workload (one 256
+    GiB file at 8 GPUs, 32 GiB shard per GPU; here --shard-gib shrinks it),
+    with the shard layout and the gather in `parallelism`."""
+    r = subprocess.run([sys.executable, BENCH, "--config", "4", "--gpus", "3", "--dist-backend", "gloo",
+                        "--shard-gib", "0.01", "--check-launch"], capture_output=True, text=True, timeout=240,
+                       env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 3 and line["multi"]["world"] == 3
+    c = line["config"]
+    assert "one 256 GiB synthetic file" in c["workload"] and "configs[3]" in c["workload"]
+    assert c["block_size"] == 4096 and c["files"] == 1
+    assert c["total_bytes"] == 3 * c["bytes_per_gpu"] and c["blocks"] == c["total_bytes"] // 4096
+    assert c["parallelism"] == "shard3+gloo_gather(pipelined, root rotating)"
+
+
 def test_dist_timeout_is_passed():
     # a stuck collective must fail the run, not hang it: the process group
     # is created with --dist-timeout (default 300 s)

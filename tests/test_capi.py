@@ -231,6 +231,73 @@ def test_file_blocks_validation_without_device(tmp_path):
         host.index_file_blocks("/nonexistent/file", [0], [1])
 
 
+def test_fd_routes_validation_without_device(tmp_path):
+    """sf_index_fd_blocks / sf_index_fd_fixed (the chunker's own descriptor):
+    stamps, argument checks and the stamp comparison all run before any
+    device call.  A stamp that no longer matches the open file is SF_EAGAIN
+    (the caller re-chunks); a non-regular descriptor is SF_EINVAL."""
+    L = syncfast_amd.lib()
+    p = tmp_path / "f"
+    p.write_bytes(bytes(range(256)) * 4)
+    out = np.zeros(4, host.SIG_DTYPE)
+    pout = out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig))
+    n = ctypes.c_uint64(77)
+    with open(p, "rb") as f:
+        fd = f.fileno()
+        st = host.file_stamp(fd)
+        sb = os.fstat(fd)
+        assert (st.dev, st.ino, st.size, st.nlink) == (sb.st_dev, sb.st_ino, 1024, sb.st_nlink)
+        assert st.mtime_sec * 10**9 + st.mtime_nsec == sb.st_mtime_ns
+        assert st.ctime_sec * 10**9 + st.ctime_nsec == sb.st_ctime_ns
+        o = np.asarray([0, 1000], np.uint64)
+        s = np.asarray([1000, 25], np.uint32)
+        assert L.sf_index_fd_blocks(fd, ctypes.byref(st), o.ctypes.data, s.ctypes.data, 2, pout, None) == \
+            _lib.SF_ERANGE
+        s2 = np.asarray([10, 5], np.uint64)
+        assert L.sf_index_fd_blocks(fd, None, s2.ctypes.data, s.ctypes.data, 2, pout, None) == _lib.SF_EINVAL
+        assert L.sf_index_fd_blocks(-1, None, None, None, 0, None, None) == _lib.SF_EINVAL
+        assert L.sf_index_fd_blocks(fd, None, None, None, 1, None, None) == _lib.SF_EINVAL
+        rows, bh = host.index_fd_blocks(fd, [], [], st)
+        assert rows.size == 0 and bh == hashlib.sha1(b"").digest()
+        # cap too small: the need, nothing read
+        assert L.sf_index_fd_fixed(fd, ctypes.byref(st), 512, pout, 1, ctypes.byref(n), None) == _lib.SF_ENOSPC
+        assert n.value == 2
+        assert L.sf_index_fd_fixed(fd, None, 0, pout, 4, ctypes.byref(n), None) == _lib.SF_EINVAL
+        assert L.sf_index_fd_fixed(-1, None, 4096, pout, 4, ctypes.byref(n), None) == _lib.SF_EINVAL
+        # the file changes after the stamp: in place (same size, mtime put back), appended, replaced
+        stale = host.file_stamp(fd)
+        stale.ctime_nsec += 1  # what a write with the mtime restored leaves: only the ctime moves
+        for call in (lambda: host.index_fd_blocks(fd, [0], [10], stale),
+                     lambda: host.index_fd_fixed(fd, 4096, stale)):
+            with pytest.raises(_lib.SfError) as e:
+                call()
+            assert e.value.code == _lib.SF_EAGAIN
+        # a link added or removed moves the ctime but not the bytes: still the same file
+        moved = host.file_stamp(fd)
+        moved.nlink += 1
+        moved.ctime_nsec += 1
+        assert _lib.same_stamp(moved, host.file_stamp(fd))
+        with open(p, "ab") as w:
+            w.write(b"more")
+        with pytest.raises(_lib.SfError) as e:
+            host.index_fd_blocks(fd, [0], [10], st)
+        assert e.value.code == _lib.SF_EAGAIN
+    # an empty file: no blocks, SHA1("") -- no device needed
+    e0 = tmp_path / "empty"
+    e0.write_bytes(b"")
+    with open(e0, "rb") as f:
+        rows, bh = host.index_fd_fixed(f.fileno(), 4096, host.file_stamp(f.fileno()))
+        assert rows.size == 0 and bh == hashlib.sha1(b"").digest()
+    # a pipe is not a regular file: the list cannot be read again
+    r, w = os.pipe()
+    try:
+        assert L.sf_index_fd_blocks(r, None, None, None, 0, None, None) == _lib.SF_EINVAL
+        assert L.sf_index_fd_fixed(r, None, 4096, pout, 4, ctypes.byref(n), None) == _lib.SF_EINVAL
+    finally:
+        os.close(r)
+        os.close(w)
+
+
 def test_host_paths_without_device():
     """Without a GPU the host-memory entry points fail cleanly: the in-place
     route (>= 1 MiB) cannot page-lock, the staged route cannot set up its
@@ -390,13 +457,3 @@ def test_chained_kernel_is_the_measured_one():
     assert kernel_code_sha256(symbol=CHAINED_KERNEL) == rec["kernel_code_sha256"], \
         "the chained kernel changed: re-measure with scripts/c3_seq.sh and update the record"
 
-def test_table_kernel_is_the_measured_one():
-    # sha1_table_kernel<128, false>'s rate on content-defined lists depends on
-    # its compiled form: the committed measurement
-    # names the machine code it measured
-    import json
-    from syncfast_amd._lib import TABLE_KERNEL, kernel_code_sha256
-    with open(os.path.join(ROOT, "profiles", "r03", "cdc_prio", "table_kernel.json")) as f:
-        rec = json.load(f)
-    assert kernel_code_sha256(symbol=TABLE_KERNEL) == rec["kernel_code_sha256"], \
-        "the explicit-list kernel changed: re-measure with scripts/prio_thr.sh and update the record"

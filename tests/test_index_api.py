@@ -372,6 +372,15 @@ def _oracle_device_calls(monkeypatch):
     monkeypatch.setattr(host, "index_buffer_blocks", lambda data, offs, sizes: rows_of(bytes(data), offs, sizes))
     monkeypatch.setattr(host, "index_file_blocks",
                         lambda path, offs, sizes: rows_of(open(path, "rb").read(), offs, sizes))
+    monkeypatch.setattr(host, "index_fd_blocks",
+                        lambda fd, offs, sizes, stamp=None: rows_of(_pread_all(fd), offs, sizes))
+
+
+def _pread_all(fd):
+    """The whole file open on fd, read with pread (the descriptor's position
+    is the chunker's, as in the library)."""
+    size = os.fstat(fd).st_size
+    return os.pread(fd, size, 0) if size else b""
 
 
 def _tree(root, seed):
@@ -433,13 +442,13 @@ def test_fixed_rows_need_the_offset_size_reader(tmp_path, monkeypatch):
     data = oracle.splitmix_bytes(20_000, 4100).tobytes()
     (root / "f").write_bytes(data)
 
-    def fake_index_file(path, bs):
-        offs, sizes, dig = oracle.index_fixed(np.frombuffer(open(path, "rb").read(), np.uint8), bs)
+    def fake_index_fd_fixed(fd, bs, stamp=None):
+        offs, sizes, dig = oracle.index_fixed(np.frombuffer(_pread_all(fd), np.uint8), bs)
         rows = np.zeros(len(offs), host.SIG_DTYPE)
         rows["offset"], rows["size"], rows["sha1"] = offs, sizes, dig
         return rows, oracle.blocks_hash(dig)
 
-    monkeypatch.setattr(host, "index_file", fake_index_file)
+    monkeypatch.setattr(host, "index_fd_fixed", fake_index_fd_fixed)
     idx = Index.open_in_memory(chunker=FixedChunker(4096))
     idx.index_file(root / "f", "f")
     rows = idx.list_file_blocks(idx.get_file("f")[0])
@@ -473,8 +482,9 @@ def test_read_block_short_file(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", [False, True])
 def test_boundary_rows_read_back_on_the_gpu(gpu, tmp_path, stream):
-    """The same through the real device calls: sf_index_file_blocks (the
-    chunker streamed the open file, the library re-reads it by windows) and
+    """The same through the real device calls: sf_index_fd_blocks (the
+    chunker streamed the open file, the library re-reads that descriptor by
+    windows) and
     sf_index_buffer_blocks (the bytes in memory)."""
     root = tmp_path / "tree"
     files = _tree(root, 4200)

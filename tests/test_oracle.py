@@ -103,3 +103,25 @@ def test_adler_oracle_matches_zlib():
         assert oracle.adler_fixed(data, bs).tolist() == want
     offs, sizes = [0, 17, 1000, 299_990], [0, 5000, 64, 10]
     assert oracle.adler_blocks(data, offs, sizes).tolist() == [zlib.adler32(data[o:o + s]) for o, s in zip(offs, sizes)]
+
+
+def test_zpaq_standin_is_the_surveys_restatement():
+    """The configs[0] stand-in chunker (examples/zpaq_standin.h, timed by
+    bench.py's config1 block) is zpaq's fragmenter in the survey's form: on
+    the reference KAT input it cuts at 5,908 / 6,547 / 14,382 (SURVEY.md
+    Appendix A, "Restatement that failed") -- NOT the crate's 11,579 /
+    44,347 (src/index.rs:765-786), which is why it is only a cost stand-in.
+    Its single pass (each block SHA-1'd as it is cut) equals hashlib per
+    block, scalar and SHA-NI."""
+    import hashlib
+    kat = oracle.kat_input()
+    sizes = oracle.zpaq_standin_sizes(kat)
+    assert list(np.cumsum(sizes)[:3]) == [5908, 6547, 14382] and int(sizes.sum()) == len(kat)
+    data = oracle.splitmix_bytes(3 << 20, 0x5EED0000)
+    sizes = oracle.zpaq_standin_sizes(data)
+    assert sizes.max() <= 32768 and sizes.min() >= 1 and int(sizes.sum()) == data.size
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    want = np.stack([np.frombuffer(hashlib.sha1(data[o:o + s].tobytes()).digest(), np.uint8)
+                     for o, s in zip(offs, sizes.astype(np.int64))])
+    for shani in (False, True):
+        assert np.array_equal(oracle.zpaq_standin_index(data, shani), want)
