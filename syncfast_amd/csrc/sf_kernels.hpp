@@ -37,6 +37,20 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // raw buffer, gfx9 family
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // ---------------------------------------------------------- wave helpers
+// The lane index.  A build with SF_OPAQUE_LANE reads it through an asm
+// statement the compiler cannot move, so that nothing derived from it is
+// hoisted out of a loop around a whole group (the persistent form of the
+// explicit-list kernel, whose loop otherwise keeps both hash paths' lane
+// addresses live across the other path).
+__device__ __forceinline__ int lane_id() {
+#ifdef SF_OPAQUE_LANE
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+#else
+  return threadIdx.x & 63;
+#endif
+}
 // A value identical in every lane, moved to SGPRs so that everything derived
 // from it (buffer resources, loop bounds) stays scalar.
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
@@ -157,7 +171,7 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
   constexpr int GSHIFT = PIECES == 4 ? 2 : (PIECES == 8 ? 1 : 0);
   constexpr int BLK_PER_DMA = 1024 / TILE;    // blocks covered by one DMA wave-instruction
   static_assert(PIECES == 4 || PIECES == 8 || PIECES == 16, "TILE must be 64, 128 or 256");
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
 
   st.init();
   if constexpr (WEAK) wk.init();
@@ -393,7 +407,7 @@ template <int TILE, bool WEAK>
 __device__ __forceinline__ void fixed_wave(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs,
                                            uint64_t nblocks, uint8_t* __restrict__ digests, const PadSchedule pad,
                                            uint32_t* __restrict__ weak, uint64_t wave, uint4* __restrict__ tile) {
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   const uint64_t first = wave * 64;  // this wave's 64 consecutive blocks
   if (first >= nblocks) return;
   const uint64_t blk = first + lane;
@@ -475,7 +489,7 @@ __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uin
                                            const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
                                            uint8_t* __restrict__ out, int* __restrict__ status,
                                            uint32_t spin_limit) {
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   Sha1 st;
   st.init();
   const uint8_t* p = runs + (uint64_t)(valid ? f : 0) * run_stride;
@@ -545,7 +559,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 // [lo, hi) of each lane's run; part 0/2 then the padding chunk(s).
 __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave, uint4* __restrict__ tile) {
   __builtin_amdgcn_s_setprio(SF_CHAIN_PRIO);  // latency-bound chains issue first on a shared SIMD
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   const uint32_t f = wave * 64 + lane;
   const bool valid = f < j.files;
   Sha1 st;
@@ -622,7 +636,7 @@ sha1_fixed2_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, 
                    uint8_t* __restrict__ digests, const PadSchedule pad) {
   constexpr int TILE = 64, PIECES = 4;
   __shared__ uint4 smem[kWavesPerWG * 128 * PIECES];
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 128;
   if (first >= nblocks) return;
@@ -717,7 +731,7 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
                    uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
                    int* __restrict__ status, uint32_t spin_limit) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t per_stage = rows * m;
   if (blockIdx.x < chain_wgs) {
@@ -856,7 +870,7 @@ __device__ __forceinline__ void list_read(uint32_t (&d)[36], const uint4* myq) {
 __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data, uint64_t off, uint32_t size,
                                                bool valid, uint64_t base, uint64_t span, uint4* __restrict__ wave_tile,
                                                Sha1& st) {
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   st.init();
   // compressions of this lane's message (the slot path's blocks are < 3.75
   // GiB, so the 32-bit form cannot wrap; the wide form cost 5 spilled VGPRs)
@@ -922,7 +936,7 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
 #define SF_TABLE_WG 4  // waves per workgroup (A/B: 1, 2)
 #endif
 #ifndef SF_TABLE_PERSIST
-#define SF_TABLE_PERSIST 0  // 1: persistent waves claiming groups (A/B record, slower)
+#define SF_TABLE_PERSIST 0  // 1: persistent waves claiming groups; 2: + generation priority (A/B records)
 #endif
 
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
@@ -939,7 +953,7 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
                                             uint64_t nblocks, uint8_t* __restrict__ digests, int* __restrict__ status,
                                             uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
                                             uint64_t g, uint4* __restrict__ tile) {
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   const uint64_t first = g * 64;
   bool valid = first + lane < nblocks;
   const uint64_t blk = (order && valid) ? (uint64_t)order[first + lane] : first + lane;
@@ -1052,10 +1066,15 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
 //     kept for the record) lose that: a wave's age is its launch, not its
 //     group's, so an old wave that keeps claiming groups starves a younger
 //     neighbour, whose group then ends last (2501 vs 3031 GiB/s);
-//   * what is left is the end of the launch: a SIMD idles once its last
-//     waves are done, and with four-wave workgroups a slot is handed out
-//     again only when all four are (SF_TABLE_WG).
-// next_group (SF_TABLE_PERSIST=1 builds only): the claim counter.
+//   * what is left is the end of the launch: the SIMDs' last waves end
+//     over ~8 % of the span (traces: last end min / median / max 1225 /
+//     1303 / 1406 us), since a slot freed late may take a group queued
+//     behind two older ones.  Persistent waves with the claim's generation
+//     as priority (SF_TABLE_PERSIST=2; SF_OPAQUE_LANE keeps a 3-wave build
+//     to 80 spilled bytes, all outside the step loops) end within 3 %, but
+//     issue slower while busy; every form measured sits within +-3 % of
+//     this one on the content-defined list.
+// next_group (SF_TABLE_PERSIST builds only): the claim counter.
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(64 * SF_TABLE_WG, SF_TABLE_LB)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
@@ -1074,8 +1093,10 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
     if ((threadIdx.x & 63) == 0) k = __hip_atomic_fetch_add(next_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return __builtin_amdgcn_readfirstlane(k);
   };
-  uint32_t g = next_group ? claim() : blockIdx.x * SF_TABLE_WG + wid;
+  // a wave's first group is its launch index; later ones come from the
+  // counter (zeroed by the sort), numbered on from the launch
   const uint32_t launched = gridDim.x * SF_TABLE_WG;
+  uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
   while (g < ngroups) {  // one call site: the group body is inlined once
 #if SF_TABLE_PERSIST == 2
     // groups issue in claim order, not in their waves' launch order: the
@@ -1090,7 +1111,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 #endif
     table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
     if (!next_group) break;
-    g = claim();
+    g = launched + claim();
   }
 #else
   (void)next_group;
