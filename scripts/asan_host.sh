@@ -45,6 +45,7 @@ run wire -w 104857601 -b 4096 || rc=1
 run wire_bs1000 -w 3000001 -b 1000 || rc=1
 run lookup -L -b 4096 "$W"/f09 "$W"/f09 || rc=1
 run cdc -C "$W"/f0* || rc=1
+run zpaq -Z "$W"/f0* || rc=1  # default splice: stamp + stand-in chunker + sf_index_fd_blocks
 run wire_cdc -v 20000001 || rc=1
 # every route over the same files gives the same rows and blocks_hash
 for m in buffer shards inplace inplace_bounce; do
