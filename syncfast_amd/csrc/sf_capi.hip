@@ -166,8 +166,8 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.
 // kernels, ~21 us for 0.5 M blocks, against ~56 us of GPU time for rocprim's
 // radix sort with its key kernel; profiles/r03/sort/); wider keys (the
 // SF_TABLE_CLASS_BITS A/B knob) keep rocprim.
-// *counter: a device word of the same workspace set to 0 on `s` (the
-// persistent table kernel's group counter).
+// *counter: kTableCtrWords device words of the same workspace set to 0 on
+// `s` (the claim counter of the table kernel's persistent A/B forms).
 // Returns nullptr (unsorted launch) if anything fails.
 uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out, uint32_t** counter) {
   *ws_out = nullptr;
@@ -187,7 +187,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
 #define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
 #endif
   if (SF_CLASS_SORT && kbits == 8) {  // the default: one counting pass over 256 classes (sf_sort.hip)
-    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n)), total = ob + cb + 256;
+    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n)), total = ob + cb + 4 * sfi::kTableCtrWords;
     uint8_t* ws = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
       (void)hipGetLastError();
@@ -195,7 +195,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
     }
     uint32_t* order = reinterpret_cast<uint32_t*>(ws);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + ob + cb);
-    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, ctr, s) != SF_OK) {
+    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, ctr, sfi::kTableCtrWords, s) != SF_OK) {
       (void)hipGetLastError();
       (void)hipFreeAsync(ws, s);
       return nullptr;
@@ -211,14 +211,14 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
     (void)hipGetLastError();
     return nullptr;
   }
-  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp) + 256;
+  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp) + 4 * sfi::kTableCtrWords;
   uint8_t* ws = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
   uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + 2 * kb + 2 * ib + up(tmp));
-  if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) != hipSuccess) {
+  if (hipMemsetAsync(ctr, 0, 4 * sfi::kTableCtrWords, s) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipFreeAsync(ws, s);
     return nullptr;

@@ -279,9 +279,13 @@ int launch_table_kernel(bool weak_form, unsigned grid, const uint8_t* d_data, ui
                         const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests,
                         int* d_status, uint32_t* weak, const uint32_t* order, uint32_t* next_group, unsigned cus,
                         hipStream_t stream);
-// zero_word (may be NULL): a device word the sort sets to 0, stream-ordered
-// (the persistent table kernel's group counter).
+// zero_words (may be NULL): n_zero device words the sort sets to 0,
+// stream-ordered (the claim counter of the table kernel's persistent A/B
+// forms, kTableCtrWords).
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
-                uint32_t* zero_word, hipStream_t s);
+                uint32_t* zero_words, uint32_t n_zero, hipStream_t s);
+// The table kernel's counter block: word 0 the claim counter (a 256-B block,
+// so that an A/B form can keep more state beside it).
+constexpr uint32_t kTableCtrWords = 64;
 
 }  // namespace sfi

@@ -935,6 +935,12 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
 #ifndef SF_TABLE_WG
 #define SF_TABLE_WG 4  // waves per workgroup (A/B: 1, 2)
 #endif
+#ifndef SF_TABLE_SNAKE
+#define SF_TABLE_SNAKE 2  // bit r: wave round r takes its groups in reverse (0: none, A/B)
+#endif
+#ifndef SF_TABLE_ROUND
+#define SF_TABLE_ROUND 1024u  // waves per round: MI355X's SIMDs (256 CUs x 4)
+#endif
 #ifndef SF_TABLE_PERSIST
 #define SF_TABLE_PERSIST 0  // 1: persistent waves claiming groups; 2: + generation priority (A/B records)
 #endif
@@ -1115,7 +1121,23 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
   }
 #else
   (void)next_group;
-  const uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
+  uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
+#if SF_TABLE_SNAKE
+  // The first rounds of waves land one per SIMD per round (wave w and
+  // w + SF_TABLE_ROUND on the same SIMD, traces of round 4), so in the
+  // sort's order SIMD i would start with groups i, R + i and 2R + i: the
+  // longest group of every round on the same SIMDs (first-round work per
+  // SIMD 589..967 compressions, mean 764, on the CDC-like list).  Round 1
+  // takes its groups in reverse, pairing the longest of round 0 with the
+  // shortest of round 1.  Bit r of SF_TABLE_SNAKE reverses round r.  R is
+  // MI355X's 1024 SIMDs at compile time: a runtime R moved this kernel's
+  // compiled form and cost the 4 KiB list 6 % (profiles/r04/s18/); on a
+  // device with fewer SIMDs the reversal is one harmless permutation.
+  if (order) {
+    const uint32_t R = SF_TABLE_ROUND, r = g / R;
+    if (r < 8 && ((SF_TABLE_SNAKE >> r) & 1u) && (r + 1) * R <= ngroups) g = r * R + (R - 1u - g % R);
+  }
+#endif
   if (g < ngroups) table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
 #endif
 }

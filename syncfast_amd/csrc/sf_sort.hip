@@ -68,9 +68,10 @@ class_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits
 // place, and the bin's total.
 __global__ void __launch_bounds__(kSortThreads)
 class_scan_kernel(uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ totals,
-                  uint32_t* __restrict__ zero_word) {
+                  uint32_t* __restrict__ zero_words, uint32_t n_zero) {
   __shared__ uint32_t wsum[kSortThreads / 64];
-  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;  // the table kernel's group counter
+  if (zero_words && blockIdx.x == 0)  // the table kernel's counters
+    for (uint32_t i = threadIdx.x; i < n_zero; i += kSortThreads) zero_words[i] = 0u;
   uint32_t* col = hist + (uint64_t)blockIdx.x * ntiles;
   uint32_t carry = 0;
   for (uint32_t t0 = 0; t0 < ntiles; t0 += kSortThreads) {
@@ -152,7 +153,7 @@ size_t class_order_workspace(uint64_t n) {
 }
 
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
-                uint32_t* zero_word, hipStream_t s) {
+                uint32_t* zero_words, uint32_t n_zero, hipStream_t s) {
   if (n == 0) return SF_OK;
   if (n > 0xFFFFFFFFull || kmax >= sf::kSortBins) return SF_EINVAL;
   const uint32_t ntiles = (uint32_t)((n + sf::kSortTile - 1) / sf::kSortTile);
@@ -161,7 +162,7 @@ int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t km
   hipLaunchKernelGGL(sf::class_hist_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
                      hist, ntiles);
   hipLaunchKernelGGL(sf::class_scan_kernel, dim3(sf::kSortBins), dim3(sf::kSortThreads), 0, s, hist, ntiles,
-                     totals, zero_word);
+                     totals, zero_words, n_zero);
   hipLaunchKernelGGL(sf::class_scatter_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
                      hist, totals, ntiles, d_order);
   return hip_err(hipGetLastError());
@@ -175,7 +176,7 @@ extern "C" int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t
   hipStream_t s = static_cast<hipStream_t>(stream);
   void* ws = nullptr;
   if (hipMallocAsync(&ws, sfi::class_order_workspace(n), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
-  const int rc = sfi::class_order(d_sizes, n, 4, 255, ws, d_order, nullptr, s);
+  const int rc = sfi::class_order(d_sizes, n, 4, 255, ws, d_order, nullptr, 0, s);
   (void)hipFreeAsync(ws, s);
   return rc;
 }
