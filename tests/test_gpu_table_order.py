@@ -161,6 +161,24 @@ def test_default_sort_large_cdc_list(gpu, knobs):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
 
 
+@pytest.mark.parametrize("nblocks", [64 * 2047, 64 * 2048 - 1, 64 * 2048, 64 * 2048 + 1, 64 * 3072 + 5])
+def test_sorted_round_reversal_edges(gpu, knobs, nblocks):
+    # wave round 1 (groups 1024..2047 of the sorted order) takes its groups
+    # in reverse when the launch holds it whole (SF_TABLE_SNAKE): lists just
+    # below, at and above 2048 groups, small blocks of every class, every
+    # digest at its own index = the oracle
+    knobs.set("SF_TEST_TABLE_SORT", 1)
+    rng = np.random.default_rng(38_000 + nblocks)
+    sizes = rng.integers(0, 600, nblocks).astype(np.int64)
+    n = int(sizes.sum()) + 64
+    data = oracle.splitmix_bytes(n, 48_000 + nblocks)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64) + int(rng.integers(0, 64))
+    t = _dev(data, gpu, 3)
+    got = device.index_device_blocks(t, torch.from_numpy(offs).to(gpu),
+                                     torch.from_numpy(sizes.astype(np.int32)).to(gpu)).cpu().numpy()
+    assert np.array_equal(got, oracle.index_blocks(data, offs, sizes)), nblocks
+
+
 def _class_keys(sizes):
     """length_class(n_chunks(size), 4 mantissa bits) clamped at 255
     (sf_kernels.hpp), in numpy."""
