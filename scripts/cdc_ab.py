@@ -121,9 +121,14 @@ def main():
     torch.cuda.synchronize()
     names = list(lists) + ([] if only else ["fixed4k"])
     times = {(i, k): [] for i in range(len(libs)) for k in names}
+    # the library measured first after another list runs ~3 % slow on the
+    # 4 KiB list (profiles/r04/s20, s21): the order rotates every round
+    # (CDC_ROTATE=0: fixed order, as before round 4's s22)
+    rotate = os.environ.get("CDC_ROTATE", "1") == "1"
     for r in range(rounds):
         for k in names:
-            for i in range(len(libs)):
+            for j in range(len(libs)):
+                i = (j + r) % len(libs) if rotate else j
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
                 for _ in range(reps):

@@ -3,7 +3,8 @@ rocprofv3 --kernel-trace (no counters): the dispatch order is cdc_ab.py's
 (for each round, for each list, for each library, CDC_REPS calls), so every
 sha1_table_kernel launch is attributed to its library and list, with the
 sort kernels before it and the gaps around it.
-usage: python scripts/table_ktrace.py kernel_trace.csv LISTS NLIBS REPS ROUNDS"""
+usage: python scripts/table_ktrace.py kernel_trace.csv LISTS NLIBS REPS ROUNDS [rot]
+(rot: cdc_ab.py rotated the library order every round, its default since s22)"""
 import csv
 import statistics
 import sys
@@ -12,6 +13,7 @@ import sys
 def main():
     path, lists, nlibs, reps, rounds = sys.argv[1], sys.argv[2].split(","), int(sys.argv[3]), int(sys.argv[4]), \
         int(sys.argv[5])
+    rot = len(sys.argv) > 6 and sys.argv[6] == "rot"
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     calls, cur, fixed = [], [], []
     for r in rows:
@@ -33,7 +35,8 @@ def main():
     i = 0
     for _r in range(rounds):
         for k in lists:
-            for lib in range(nlibs):
+            for pos in range(nlibs):
+                lib = (pos + _r) % nlibs if rot else pos
                 for _ in range(reps):
                     c = calls[i]
                     i += 1

@@ -988,12 +988,15 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
                ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 #ifndef SF_TABLE_PRIO
-#define SF_TABLE_PRIO 1  // 0: no critical-path priority (A/B)
+#define SF_TABLE_PRIO 0  // 1: critical-path priority (round 3; A/B record since the round-1 pairing)
 #endif
 #if SF_TABLE_PRIO && !SF_TABLE_PERSIST
   // Critical-path priority (round 3): a sorted group longer than the list's
   // compressions per lane of 3 waves on 1024 SIMDs (len / 64 + nblocks: exact
-  // for a list that tiles the data once) issues at priority 2.
+  // for a list that tiles the data once) issues at priority 2.  Off since the
+  // first round's pairing (SF_TABLE_SNAKE): with it the build without the
+  // priority ran the CDC-like list 0.6-1.2 % faster in two order-rotated
+  // sessions, the 4 KiB list the same (profiles/r04/s20, s21).
   if (order && (uint64_t)geo.max_nch * (64ull * 3 * 1024) >= len / 64 + nblocks) __builtin_amdgcn_s_setprio(2);
 #endif
 #ifdef SF_WAVE_TRACE
