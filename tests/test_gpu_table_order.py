@@ -179,6 +179,21 @@ def test_sorted_round_reversal_edges(gpu, knobs, nblocks):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes)), nblocks
 
 
+def test_sorted_round_reversal_weak(gpu, knobs):
+    # the weak-sum form of the kernel maps its waves the same way
+    knobs.set("SF_TEST_TABLE_SORT", 1)
+    nblocks = 64 * 2048 + 77
+    rng = np.random.default_rng(39_000)
+    sizes = rng.integers(0, 600, nblocks).astype(np.int64)
+    n = int(sizes.sum())
+    data = oracle.splitmix_bytes(n, 49_000)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    dig, weak = device.index_device_blocks_weak(_dev(data, gpu), torch.from_numpy(offs).to(gpu),
+                                                torch.from_numpy(sizes.astype(np.int32)).to(gpu))
+    assert np.array_equal(dig.cpu().numpy(), oracle.index_blocks(data, offs, sizes))
+    assert np.array_equal(weak.cpu().numpy().view(np.uint32), oracle.adler_blocks(data, offs, sizes))
+
+
 def _class_keys(sizes):
     """length_class(n_chunks(size), 4 mantissa bits) clamped at 255
     (sf_kernels.hpp), in numpy."""
