@@ -38,6 +38,11 @@ int sf_test_get_stat(const char* name, int64_t* value);
  * Asynchronous on `stream`; SF_EINVAL for n >= 2^32. */
 int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream);
 
+/* The same with `mbits` mantissa bits (1..6) of the length class: the key
+ * is clamped at (16 << max(mbits, 4)) - 1 (8, 9 or 10 bits), as the
+ * SF_TABLE_CLASS_BITS knob sorts.  SF_EINVAL for mbits outside 1..6. */
+int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t* d_order, void* stream);
+
 /* Called by the descriptor and path routes that pread a regular file
  * (sf_index_fd_blocks, sf_index_fd_fixed, sf_index_file_blocks,
  * sf_index_file) after each window has been read, on the calling thread,

@@ -40,6 +40,7 @@ EXPORTED = (
 # Test hooks (include/syncfast_amd_test.h): knobs latched at load, route counters,
 # the explicit-list processing order.
 EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat", "sf_test_table_order",
+                 "sf_test_table_order_bits",
                  "sf_test_set_read_hook")
 
 
@@ -135,6 +136,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_test_get_knob.argtypes = [ctypes.c_char_p, pi64]
     L.sf_test_get_stat.argtypes = [ctypes.c_char_p, pi64]
     L.sf_test_table_order.argtypes = [vp, u64, vp, vp]
+    L.sf_test_table_order_bits.argtypes = [vp, u64, ctypes.c_uint32, vp, vp]
     L.sf_test_set_read_hook.argtypes = [READ_HOOK, vp]
     for name in EXPORTED + EXPORTED_TEST:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):

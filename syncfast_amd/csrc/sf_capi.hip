@@ -162,10 +162,10 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.
 // then alike in length AND close together in memory; a class-bucketing by
 // atomics scattered each class's blocks across the buffer and the list ran
 // at half the rate (1410 vs 2609 GiB/s on one box, profiles/r03/bucket_sort_rejected/).
-// The default 8-bit key takes the counting sort of sf_sort.hip (three
-// kernels, ~21 us for 0.5 M blocks, against ~56 us of GPU time for rocprim's
-// radix sort with its key kernel; profiles/r03/sort/); wider keys (the
-// SF_TABLE_CLASS_BITS A/B knob) keep rocprim.
+// The key takes the counting sort of sf_sort.hip (three kernels, ~21 us for
+// 0.5 M blocks with the default 8-bit key, against ~56 us of GPU time for
+// rocprim's radix sort with its key kernel; profiles/r03/sort/), the 9- and
+// 10-bit keys of the SF_TABLE_CLASS_BITS knob too (512 / 1024 bins).
 // *counter: kTableCtrWords device words of the same workspace set to 0 on
 // `s` (the claim counter of the table kernel's persistent A/B forms).
 // Returns nullptr (unsorted launch) if anything fails.
@@ -173,20 +173,23 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   *ws_out = nullptr;
   *counter = nullptr;
   // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
+#ifdef SF_CLASS_BITS_FORCE
+  const uint32_t mbits = SF_CLASS_BITS_FORCE;  // A/B builds (make variant EXTRA=-DSF_CLASS_BITS_FORCE=5)
+#else
   const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
+#endif
 
-  // classes < 32 << mbits; with 4 mantissa bits (the default) the key is
-  // clamped to 8 bits (every block of 2^16+ compressions, i.e. >= 4 MiB,
-  // shares the top class) and one radix pass sorts it: ~25 us saved per
-  // call against the 11-bit key of 6 mantissa bits, which the DMA path does
-  // not need (class width 6.25 % vs 1.6 %, profiles/r03/).
-  const unsigned kbits = mbits <= 4 ? 8u : 5u + mbits;
+  // classes < 32 << mbits; the key is clamped at (16 << mbits) - 1, so every
+  // block of 2^16+ compressions (>= 4 MiB) shares the top class: 8 bits with
+  // 4 mantissa bits (the default; class width 6.25 %), 9 with 5, 10 with 6
+  // (1.6 %), all one counting pass of sf_sort.hip.
+  const unsigned kbits = mbits <= 4 ? 8u : 4u + mbits;
   const uint32_t kmax = (1u << kbits) - 1u;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
 #ifndef SF_CLASS_SORT
 #define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
 #endif
-  if (SF_CLASS_SORT && kbits == 8) {  // the default: one counting pass over 256 classes (sf_sort.hip)
+  if (SF_CLASS_SORT && kbits <= 10) {  // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
     const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n)), total = ob + cb + 4 * sfi::kTableCtrWords;
     uint8_t* ws = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {

@@ -1146,8 +1146,8 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
 }
 
 // Sort keys of an explicit block list for sha1_table_kernel's `order` (the
-// rocprim form, kept for the wider keys of the SF_TABLE_CLASS_BITS A/B knob;
-// the default 4 mantissa bits take the counting sort of sf_sort.hip): the
+// rocprim form, kept for SF_CLASS_SORT=0 builds; every class width of the
+// SF_TABLE_CLASS_BITS knob takes the counting sort of sf_sort.hip): the
 // block's compression count on a log scale with `mbits` mantissa bits
 // (classes 6.25 % wide with 4 bits, exact below 16; the key is clamped to
 // kmax = 255, so every block of >= 2^16 compressions shares the top class),

@@ -1,7 +1,8 @@
 // sf_sort.hip -- the processing order of an explicit block list for
 // sha1_table_kernel: a stable counting sort of the
-// blocks by their 8-bit length class, descending (list order within a
-// class), in three small kernels.  It replaces a general radix sort that
+// blocks by their length class (8-bit by default; 9 and 10 bits for the
+// SF_TABLE_CLASS_BITS A/B), descending (list order within a class), in three
+// small kernels.  It replaces a general radix sort that
 // spent ~45 us per call (key kernel, three buffer fills, histogram and
 // onesweep passes) on what is one pass over 256 bins.
 //
@@ -20,7 +21,7 @@ namespace sf {
 constexpr int kSortThreads = 256;
 constexpr int kSortRounds = 8;
 constexpr uint32_t kSortTile = kSortThreads * kSortRounds;  // blocks per tile
-constexpr uint32_t kSortBins = 256;                          // 8-bit class keys
+constexpr uint32_t kSortBinsMax = 1024;                      // 8- to 10-bit class keys
 
 __device__ __forceinline__ uint32_t class_key(uint32_t size, uint32_t mbits, uint32_t kmax) {
   const uint32_t k = length_class(n_chunks_wide(size), mbits);
@@ -47,12 +48,17 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t* wsum, ui
 }
 
 // 1. Class histogram of every tile, bin-major: hist[bin * ntiles + tile].
+// BINS: 256, 512 or 1024 classes (8-, 9- or 10-bit keys); each of the 256
+// threads owns BINS / 256 of them.
+template <uint32_t BINS>
 __global__ void __launch_bounds__(kSortThreads)
 class_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t kmax,
                   uint32_t* __restrict__ hist, uint32_t ntiles) {
-  __shared__ uint32_t h[kSortBins];
+  constexpr uint32_t BPT = BINS / kSortThreads;
+  __shared__ uint32_t h[BINS];
   const uint32_t tid = threadIdx.x, tile = blockIdx.x;
-  h[tid] = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < BPT; ++j) h[tid * BPT + j] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)tile * kSortTile;
 #pragma unroll
@@ -61,7 +67,8 @@ class_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits
     if (i < n) atomicAdd(&h[class_key(sizes[i], mbits, kmax)], 1u);
   }
   __syncthreads();
-  hist[(uint64_t)tid * ntiles + tile] = h[tid];
+#pragma unroll
+  for (uint32_t j = 0; j < BPT; ++j) hist[(uint64_t)(tid * BPT + j) * ntiles + tile] = h[tid * BPT + j];
 }
 
 // 2. Per bin (one workgroup each): exclusive prefix over the tiles, in
@@ -88,23 +95,36 @@ class_scan_kernel(uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __rest
 // 3. Scatter: block i goes to order[pos], pos = (blocks of higher classes)
 // + (blocks of its class in earlier tiles) + (its rank in its tile: earlier
 // rounds, earlier waves of its round, lower lanes of its wave).
+template <uint32_t BINS>
 __global__ void __launch_bounds__(kSortThreads)
 class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits, uint32_t kmax,
                      const uint32_t* __restrict__ hist, const uint32_t* __restrict__ totals, uint32_t ntiles,
                      uint32_t* __restrict__ order) {
   constexpr int kWaves = kSortThreads / 64;
-  __shared__ uint32_t running[kSortBins];
-  __shared__ uint32_t wcnt[kWaves][kSortBins];
+  constexpr uint32_t BPT = BINS / kSortThreads;
+  constexpr int KBITS = BINS == 256 ? 8 : BINS == 512 ? 9 : 10;
+  __shared__ uint32_t running[BINS];
+  __shared__ uint32_t wcnt[kWaves][BINS];
   __shared__ uint32_t wsum[kWaves];
   const uint32_t tid = threadIdx.x, tile = blockIdx.x;
   const int lane = tid & 63, w = tid >> 6;
-  // classes in descending order: bin b starts after every bin above it
-  const uint32_t tb = totals[kSortBins - 1 - tid];  // thread t holds bin 255 - t
-  uint32_t all;
-  const uint32_t above = block_scan256(tb, wsum, &all) - tb;
-  running[kSortBins - 1 - tid] = above + hist[(uint64_t)(kSortBins - 1 - tid) * ntiles + tile];
+  // classes in descending order: bin b starts after every bin above it;
+  // thread t holds bins BINS - 1 - (t * BPT + j), j < BPT
+  uint32_t tb = 0;
 #pragma unroll
-  for (int i = 0; i < kWaves; ++i) wcnt[i][tid] = 0;
+  for (uint32_t j = 0; j < BPT; ++j) tb += totals[BINS - 1 - (tid * BPT + j)];
+  uint32_t all;
+  uint32_t above = block_scan256(tb, wsum, &all) - tb;
+#pragma unroll
+  for (uint32_t j = 0; j < BPT; ++j) {
+    const uint32_t b = BINS - 1 - (tid * BPT + j);
+    running[b] = above + hist[(uint64_t)b * ntiles + tile];
+    above += totals[b];
+  }
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i)
+#pragma unroll
+    for (uint32_t j = 0; j < BPT; ++j) wcnt[i][tid * BPT + j] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)tile * kSortTile;
   const uint64_t lt = (1ull << lane) - 1ull;  // lanes below this one
@@ -112,10 +132,10 @@ class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mb
     const uint64_t i = base + (uint64_t)r * kSortThreads + tid;
     const bool valid = i < n;
     const uint32_t k = valid ? class_key(sizes[i], mbits, kmax) : 0u;
-    // lanes of this wave holding the same key: AND of 8 bit-plane ballots
+    // lanes of this wave holding the same key: AND of the key's bit-plane ballots
     uint64_t eq = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < KBITS; ++b) {
       const uint64_t m = __ballot((k >> b) & 1u);
       eq &= ((k >> b) & 1u) ? m : ~m;
     }
@@ -129,14 +149,16 @@ class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mb
       for (int v = 0; v < w; ++v) pos += wcnt[v][k];
     }
     __syncthreads();  // every lane has read running / wcnt
-    {
+#pragma unroll
+    for (uint32_t j = 0; j < BPT; ++j) {
+      const uint32_t b = tid * BPT + j;
       uint32_t add = 0;
 #pragma unroll
       for (int v = 0; v < kWaves; ++v) {
-        add += wcnt[v][tid];
-        wcnt[v][tid] = 0;
+        add += wcnt[v][b];
+        wcnt[v][b] = 0;
       }
-      running[tid] += add;
+      running[b] += add;
     }
     __syncthreads();
     if (valid) order[pos] = (uint32_t)i;
@@ -149,34 +171,53 @@ namespace sfi {
 
 size_t class_order_workspace(uint64_t n) {
   const uint64_t ntiles = (n + sf::kSortTile - 1) / sf::kSortTile;
-  return (size_t)(ntiles * sf::kSortBins + sf::kSortBins) * 4;
+  return (size_t)(ntiles * sf::kSortBinsMax + sf::kSortBinsMax) * 4;
+}
+
+template <uint32_t BINS>
+static void class_order_launch(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, uint32_t* hist,
+                               uint32_t ntiles, uint32_t* d_order, uint32_t* zero_words, uint32_t n_zero,
+                               hipStream_t s) {
+  uint32_t* totals = hist + (uint64_t)ntiles * BINS;
+  hipLaunchKernelGGL(sf::class_hist_kernel<BINS>, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
+                     hist, ntiles);
+  hipLaunchKernelGGL(sf::class_scan_kernel, dim3(BINS), dim3(sf::kSortThreads), 0, s, hist, ntiles, totals, zero_words,
+                     n_zero);
+  hipLaunchKernelGGL(sf::class_scatter_kernel<BINS>, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits,
+                     kmax, hist, totals, ntiles, d_order);
 }
 
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
                 uint32_t* zero_words, uint32_t n_zero, hipStream_t s) {
   if (n == 0) return SF_OK;
-  if (n > 0xFFFFFFFFull || kmax >= sf::kSortBins) return SF_EINVAL;
+  if (n > 0xFFFFFFFFull || kmax >= sf::kSortBinsMax) return SF_EINVAL;
   const uint32_t ntiles = (uint32_t)((n + sf::kSortTile - 1) / sf::kSortTile);
   uint32_t* hist = static_cast<uint32_t*>(d_ws);
-  uint32_t* totals = hist + (uint64_t)ntiles * sf::kSortBins;
-  hipLaunchKernelGGL(sf::class_hist_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
-                     hist, ntiles);
-  hipLaunchKernelGGL(sf::class_scan_kernel, dim3(sf::kSortBins), dim3(sf::kSortThreads), 0, s, hist, ntiles,
-                     totals, zero_words, n_zero);
-  hipLaunchKernelGGL(sf::class_scatter_kernel, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
-                     hist, totals, ntiles, d_order);
+  if (kmax < 256)
+    class_order_launch<256>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
+  else if (kmax < 512)
+    class_order_launch<512>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
+  else
+    class_order_launch<1024>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
   return hip_err(hipGetLastError());
 }
 
 }  // namespace sfi
 
-extern "C" int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream) {
+extern "C" int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t* d_order,
+                                        void* stream) {
+  if (mbits < 1 || mbits > 6) return SF_EINVAL;
   if (n == 0) return SF_OK;
   if (!d_sizes || !d_order || n > 0xFFFFFFFFull) return SF_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   void* ws = nullptr;
   if (hipMallocAsync(&ws, sfi::class_order_workspace(n), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
-  const int rc = sfi::class_order(d_sizes, n, 4, 255, ws, d_order, nullptr, 0, s);
+  const uint32_t kmax = (16u << (mbits < 4 ? 4 : mbits)) - 1u;
+  const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, nullptr, 0, s);
   (void)hipFreeAsync(ws, s);
   return rc;
+}
+
+extern "C" int sf_test_table_order(const uint32_t* d_sizes, uint64_t n, uint32_t* d_order, void* stream) {
+  return sf_test_table_order_bits(d_sizes, n, 4, d_order, stream);
 }

@@ -194,13 +194,14 @@ def test_sorted_round_reversal_weak(gpu, knobs):
     assert np.array_equal(weak.cpu().numpy().view(np.uint32), oracle.adler_blocks(data, offs, sizes))
 
 
-def _class_keys(sizes):
-    """length_class(n_chunks(size), 4 mantissa bits) clamped at 255
-    (sf_kernels.hpp), in numpy."""
+def _class_keys(sizes, mbits=4):
+    """length_class(n_chunks(size), mbits mantissa bits) clamped at
+    (16 << max(mbits, 4)) - 1 (sf_kernels.hpp, sf_capi.hip), in numpy."""
     nch = (sizes.astype(np.int64) + 8) // 64 + 1
     e = np.floor(np.log2(nch)).astype(np.int64)
-    k = np.where(nch < 16, nch, (e << 4) + ((nch >> np.maximum(e - 4, 0)) & 15))
-    return np.minimum(k, 255)
+    k = np.where(nch < (1 << mbits), nch,
+                 (e << mbits) + ((nch >> np.maximum(e - mbits, 0)) & ((1 << mbits) - 1)))
+    return np.minimum(k, (16 << max(mbits, 4)) - 1)
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 2047, 2048, 2049, 100_000, 1 << 20, (1 << 23) + 77])
@@ -221,4 +222,25 @@ def test_class_order_is_the_stable_descending_class_sort(gpu, n):
           "sf_test_table_order")
     got = order.cpu().numpy().view(np.uint32)
     want = np.argsort((255 - _class_keys(sizes)).astype(np.uint8), kind="stable")  # descending, stable
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mbits", [2, 5, 6])
+@pytest.mark.parametrize("n", [1, 2049, 100_000, (1 << 21) + 3])
+def test_class_order_wider_keys(gpu, n, mbits):
+    # the 9- and 10-bit keys of the SF_TABLE_CLASS_BITS knob take the same
+    # counting sort with 512 / 1024 bins
+    import ctypes
+
+    from syncfast_amd._lib import check, lib
+    rng = np.random.default_rng(39_500 + n + mbits)
+    sizes = np.concatenate([rng.geometric(1 / 8192, n // 2), rng.integers(0, 1 << 31, n - n // 2)])
+    sizes = rng.permutation(np.minimum(sizes, (1 << 31) - 1)).astype(np.uint32)
+    ts = torch.from_numpy(sizes.view(np.int32)).to(gpu)
+    order = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    check(lib().sf_test_table_order_bits(ts.data_ptr(), n, mbits, order.data_ptr(),
+                                         ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)),
+          "sf_test_table_order_bits")
+    got = order.cpu().numpy().view(np.uint32)
+    want = np.argsort(-_class_keys(sizes, mbits), kind="stable")  # descending, stable
     assert np.array_equal(got, want)
