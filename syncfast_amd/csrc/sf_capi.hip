@@ -190,7 +190,7 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
 #define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
 #endif
   if (SF_CLASS_SORT && kbits <= 10) {  // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
-    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n)), total = ob + cb + 4 * sfi::kTableCtrWords;
+    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n, kmax)), total = ob + cb + 4 * sfi::kTableCtrWords;
     uint8_t* ws = nullptr;
     if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
       (void)hipGetLastError();

@@ -267,9 +267,9 @@ inline unsigned io_threads() {
 
 // Processing order of an explicit block list (sf_sort.hip): d_order[0, n)
 // receives the block indices sorted by 8-bit length class (kmax <= 255),
-// descending, list order within a class.  d_ws: class_order_workspace(n)
+// descending, list order within a class.  d_ws: class_order_workspace(n, kmax)
 // bytes of device memory.  Stream-ordered on s.
-size_t class_order_workspace(uint64_t n);
+size_t class_order_workspace(uint64_t n, uint32_t kmax);
 // sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
 // translation unit); SF_OK or the launch error.  next_group: NULL (grid
 // workgroups, one group of 64 blocks per wave) or a zeroed device counter

@@ -172,9 +172,11 @@ class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mb
 
 namespace sfi {
 
-size_t class_order_workspace(uint64_t n) {
-  const uint64_t ntiles = (n + sf::kSortTile - 1) / sf::kSortTile;
-  return (size_t)(ntiles * sf::kSortBinsMax + sf::kSortBinsMax) * 4;
+static uint32_t sort_bins(uint32_t kmax) { return kmax < 256 ? 256u : kmax < 512 ? 512u : 1024u; }
+
+size_t class_order_workspace(uint64_t n, uint32_t kmax) {
+  const uint64_t ntiles = (n + sf::kSortTile - 1) / sf::kSortTile, bins = sort_bins(kmax);
+  return (size_t)(ntiles * bins + bins) * 4;
 }
 
 template <uint32_t BINS>
@@ -214,8 +216,8 @@ extern "C" int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uin
   if (!d_sizes || !d_order || n > 0xFFFFFFFFull) return SF_EINVAL;
   hipStream_t s = static_cast<hipStream_t>(stream);
   void* ws = nullptr;
-  if (hipMallocAsync(&ws, sfi::class_order_workspace(n), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
   const uint32_t kmax = (16u << (mbits < 4 ? 4 : mbits)) - 1u;
+  if (hipMallocAsync(&ws, sfi::class_order_workspace(n, kmax), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
   const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, nullptr, 0, s);
   (void)hipFreeAsync(ws, s);
   return rc;
