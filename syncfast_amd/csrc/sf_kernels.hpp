@@ -1075,14 +1075,15 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
 //     kept for the record) lose that: a wave's age is its launch, not its
 //     group's, so an old wave that keeps claiming groups starves a younger
 //     neighbour, whose group then ends last (2501 vs 3031 GiB/s);
-//   * what is left is the end of the launch: the SIMDs' last waves end
-//     over ~8 % of the span (traces: last end min / median / max 1225 /
-//     1303 / 1406 us), since a slot freed late may take a group queued
-//     behind two older ones.  Persistent waves with the claim's generation
-//     as priority (SF_TABLE_PERSIST=2; SF_OPAQUE_LANE keeps a 3-wave build
-//     to 80 spilled bytes, all outside the step loops) end within 3 %, but
-//     issue slower while busy; every form measured sits within +-3 % of
-//     this one on the content-defined list.
+//   * what is left is the end of the launch, and most of it is set by the
+//     first round: waves w, w + 1024 and w + 2048 land on one SIMD, so in
+//     the sort's order the same SIMDs would start with every round's
+//     longest group.  Round 1 therefore takes its groups in reverse
+//     (SF_TABLE_SNAKE, below): SIMD work max/mean 1.07 -> 1.047, the
+//     CDC-like list 2 % faster.  Persistent waves with the claim's
+//     generation as priority (SF_TABLE_PERSIST=2; SF_OPAQUE_LANE keeps a
+//     3-wave build to 80 spilled bytes, all outside the step loops) balance
+//     the end but issue slower while busy.
 // next_group (SF_TABLE_PERSIST builds only): the claim counter.
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(64 * SF_TABLE_WG, SF_TABLE_LB)
