@@ -258,13 +258,12 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
     }
     return SF_OK;
   }
-  unsigned grid = grid_for_blocks(nblocks);
+  const unsigned grid = grid_for_blocks(nblocks);
   void* ws = nullptr;
   uint32_t* counter = nullptr;
   const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws, &counter) : nullptr;
-  // A sorted list: persistent waves claiming groups in the sort's order
-  // (sha1_table_kernel; the launcher in sf_table.hip starts at most the
-  // resident ones).
+  // counter: the claim counter of the persistent A/B forms of
+  // sha1_table_kernel (SF_TABLE_PERSIST builds); the shipped launch ignores it.
   if (!order) counter = nullptr;
   const int rc = launch_table_kernel(weak != nullptr, grid, static_cast<const uint8_t*>(d_data), len, d_offsets,
                                      d_sizes, nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order,
