@@ -15,8 +15,6 @@
 #include <atomic>
 #include <vector>
 
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include "sf_internal.hpp"
 #include "sf_kernels.hpp"
 
@@ -24,16 +22,6 @@ namespace sfi __attribute__((visibility("hidden"))) {
 
 
 constexpr int kTile = 128;  // bytes of each block staged per LDS step
-#ifndef SF_FIXED_WPE
-#define SF_FIXED_WPE 1  // min waves/SIMD of the shipped fixed kernel (A/B: make variant EXTRA=-DSF_FIXED_WPE=4)
-#endif
-
-#ifdef SF_TUNING
-inline int variant_choice() {
-  const char* e = getenv("SF_VARIANT");
-  return e ? atoi(e) : 0;
-}
-#endif
 
 // Most blocks one launch takes.  HIP caps a launch at 2^32 - 1 work-items
 // (gridDim.x * blockDim.x), i.e. about 2^32 blocks at one lane per block;
@@ -96,30 +84,7 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
                        nblocks, o, pad, weak);
     return hip_err(hipGetLastError());
   }
-#ifdef SF_TUNING
-  // Tuning builds only (make variant EXTRA=-DSF_TUNING): SF_VARIANT selects a
-  // (tile, waves-per-SIMD) instantiation for interleaved A/B in one process.
-  switch (variant_choice()) {
-    case 1: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 5>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 2: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 6>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 3: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 8>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 4: hipLaunchKernelGGL((sf::sha1_fixed_kernel<64, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 5: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 4>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 6: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 2>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 7: hipLaunchKernelGGL((sf::sha1_fixed_kernel<128, 3>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-    case 8:
-      if (bs % 64 == 0 && (reinterpret_cast<uintptr_t>(d) & 15u) == 0) {
-        hipLaunchKernelGGL(sf::sha1_fixed2_kernel, dim3((unsigned)ceil_div(ceil_div(nblocks, 128), sf::kWavesPerWG)),
-                           dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad);
-        break;
-      }
-      hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
-      break;
-    default: hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr); break;
-  }
-#else
-  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, SF_FIXED_WPE>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
-#endif
+  hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
   return hip_err(hipGetLastError());
 }
 
@@ -166,18 +131,11 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.
 // 0.5 M blocks with the default 8-bit key, against ~56 us of GPU time for
 // rocprim's radix sort with its key kernel; profiles/r03/sort/), the 9- and
 // 10-bit keys of the SF_TABLE_CLASS_BITS knob too (512 / 1024 bins).
-// *counter: kTableCtrWords device words of the same workspace set to 0 on
-// `s` (the claim counter of the table kernel's persistent A/B forms).
 // Returns nullptr (unsorted launch) if anything fails.
-uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out, uint32_t** counter) {
+uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
   *ws_out = nullptr;
-  *counter = nullptr;
   // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
-#ifdef SF_CLASS_BITS_FORCE
-  const uint32_t mbits = SF_CLASS_BITS_FORCE;  // A/B builds (make variant EXTRA=-DSF_CLASS_BITS_FORCE=5)
-#else
   const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
-#endif
 
   // classes < 32 << mbits; the key is clamped at (16 << mbits) - 1, so every
   // block of 2^16+ compressions (>= 4 MiB) shares the top class: 8 bits with
@@ -186,62 +144,21 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   const unsigned kbits = mbits <= 4 ? 8u : 4u + mbits;
   const uint32_t kmax = (1u << kbits) - 1u;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-#ifndef SF_CLASS_SORT
-#define SF_CLASS_SORT 1  // 0: rocprim radix sort for the default 8-bit key too (A/B)
-#endif
-  if (SF_CLASS_SORT && kbits <= 10) {  // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
-    const size_t ob = up(n * 4), cb = up(sfi::class_order_workspace(n, kmax)), total = ob + cb + 4 * sfi::kTableCtrWords;
-    uint8_t* ws = nullptr;
-    if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    uint32_t* order = reinterpret_cast<uint32_t*>(ws);
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + ob + cb);
-    if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, ctr, sfi::kTableCtrWords, s) != SF_OK) {
-      (void)hipGetLastError();
-      (void)hipFreeAsync(ws, s);
-      return nullptr;
-    }
-    *ws_out = ws;
-    *counter = ctr;
-    return order;
-  }
-  uint16_t *kin = nullptr, *kout = nullptr;
-  uint32_t *iin = nullptr, *iout = nullptr;
-  size_t tmp = 0;
-  if (rocprim::radix_sort_pairs_desc(nullptr, tmp, kin, kout, iin, iout, (unsigned)n, 0u, kbits, s) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  const size_t kb = up(n * 2), ib = up(n * 4), total = 2 * kb + 2 * ib + up(tmp) + 4 * sfi::kTableCtrWords;
+  // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
+  const size_t ob = up(n * 4), total = ob + up(sfi::class_order_workspace(n, kmax));
   uint8_t* ws = nullptr;
   if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + 2 * kb + 2 * ib + up(tmp));
-  if (hipMemsetAsync(ctr, 0, 4 * sfi::kTableCtrWords, s) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFreeAsync(ws, s);
-    return nullptr;
-  }
-  kin = reinterpret_cast<uint16_t*>(ws);
-  kout = reinterpret_cast<uint16_t*>(ws + kb);
-  iin = reinterpret_cast<uint32_t*>(ws + 2 * kb);
-  iout = reinterpret_cast<uint32_t*>(ws + 2 * kb + ib);
-  hipLaunchKernelGGL(sf::table_keys_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, d_sizes, n, kin, iin,
-                     mbits, kmax);
-  if (hipGetLastError() != hipSuccess ||
-      rocprim::radix_sort_pairs_desc(ws + 2 * kb + 2 * ib, tmp, kin, kout, iin, iout, (unsigned)n, 0u, kbits, s) !=
-          hipSuccess) {
+  uint32_t* order = reinterpret_cast<uint32_t*>(ws);
+  if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, s) != SF_OK) {
     (void)hipGetLastError();
     (void)hipFreeAsync(ws, s);
     return nullptr;
   }
   *ws_out = ws;
-  *counter = ctr;
-  return iout;
+  return order;
 }
 
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
@@ -258,16 +175,10 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
     }
     return SF_OK;
   }
-  const unsigned grid = grid_for_blocks(nblocks);
   void* ws = nullptr;
-  uint32_t* counter = nullptr;
-  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws, &counter) : nullptr;
-  // counter: the claim counter of the persistent A/B forms of
-  // sha1_table_kernel (SF_TABLE_PERSIST builds); the shipped launch ignores it.
-  if (!order) counter = nullptr;
-  const int rc = launch_table_kernel(weak != nullptr, grid, static_cast<const uint8_t*>(d_data), len, d_offsets,
-                                     d_sizes, nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order,
-                                     counter, device_cus(), stream);
+  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
+  const int rc = launch_table_kernel(weak != nullptr, static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes,
+                                     nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order, stream);
   if (ws) (void)hipFreeAsync(ws, stream);
   return rc;
 }
@@ -330,18 +241,10 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   const size_t wbytes = 32 * sizeof(uint32_t);
   SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
-#ifdef SF_TUNING
-  // SF_STAGED_EXP: 1 = no chain workgroups (publish only), 2 = no chains and
-  // no publish (block hashing in stage order only) -- cost breakdown only.
-  const char* xe = getenv("SF_STAGED_EXP");
-  const int exp = xe ? atoi(xe) : 0;
-#else
-  const int exp = 0;
-#endif
-  const unsigned chain_wgs = exp ? 0u : (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
+  const unsigned chain_wgs = (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
   const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
-                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, exp == 2 ? nullptr : fh, d_status,
+                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, d_status,
                      chain_spin_limit());
   int rc = hip_err(hipGetLastError());
   (void)hipFreeAsync(words, s);
@@ -589,9 +492,7 @@ int sf_index_device_batch_chained_cols(const void* d_data, uint32_t n_files, uin
   }
   const uint32_t wpf = whole ? 1u : (uint32_t)(nbf / 64), wpp = whole ? 1u : (uint32_t)((col_hi - col_lo) / 64);
   const uint64_t bwaves = whole ? ceil_div(total, 64) : (uint64_t)n_files * wpp;
-#ifndef SF_NO_CHAIN_HELPER
   if (total == 0) return launch_chain_helper(cj[0], cj[1], as_stream(stream));  // chains alone: helper waves
-#endif
   // A chain wave of the block launch stages 64 files' runs through one
   // buffer resource with 32-bit offsets (file b of the wave at b * run_len):
   // runs of 62.9 MB or more (3.1 M blocks per file) could pass 4 GiB within

@@ -55,7 +55,7 @@ sha1_chain_helper_kernel(const ChainJob j0, const ChainJob j1) {
   const uint32_t nch = n_chunks(j.run_len), data_ch = j.run_len / 64;
   const uint32_t n_data = j.hi - j.lo, n = n_data + (j.part != 1 ? nch - data_ch : 0u);  // uniform
   if (helper) {
-    constexpr int D = SF_CHAIN_DEPTH;
+    constexpr int D = kChainDepth;
     const uint4* q = reinterpret_cast<const uint4*>(p + (uint64_t)j.lo * 64);
     uint4 buf[D][4];
 #pragma unroll

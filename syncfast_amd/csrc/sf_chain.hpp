@@ -24,9 +24,7 @@ struct ChainJob {
   uint32_t files, run_len, lo, hi, part, waves;  // waves = chain waves (64 files each)
 };
 
-#ifndef SF_CHAIN_DEPTH
-#define SF_CHAIN_DEPTH 4  // 64-B chunks in flight per chain lane (A/B: make variant EXTRA=-DSF_CHAIN_DEPTH=8)
-#endif
+constexpr int kChainDepth = 4;  // 64-B chunks in flight per chain lane
 
 }  // namespace sf
 

@@ -266,26 +266,18 @@ inline unsigned io_threads() {
 }
 
 // Processing order of an explicit block list (sf_sort.hip): d_order[0, n)
-// receives the block indices sorted by 8-bit length class (kmax <= 255),
-// descending, list order within a class.  d_ws: class_order_workspace(n, kmax)
-// bytes of device memory.  Stream-ordered on s.
+// receives the block indices sorted by length class (kmax < 1024: one
+// counting pass over 256, 512 or 1024 bins), descending, list order within a
+// class.  d_ws: class_order_workspace(n, kmax) bytes of device memory.
+// Stream-ordered on s.
 size_t class_order_workspace(uint64_t n, uint32_t kmax);
-// sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
-// translation unit); SF_OK or the launch error.  next_group: NULL (grid
-// workgroups, one group of 64 blocks per wave) or a zeroed device counter
-// (persistent waves that claim groups in order: at most the waves `cus` CUs
-// hold at once are started).
-int launch_table_kernel(bool weak_form, unsigned grid, const uint8_t* d_data, uint64_t len,
-                        const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests,
-                        int* d_status, uint32_t* weak, const uint32_t* order, uint32_t* next_group, unsigned cus,
-                        hipStream_t stream);
-// zero_words (may be NULL): n_zero device words the sort sets to 0,
-// stream-ordered (the claim counter of the table kernel's persistent A/B
-// forms, kTableCtrWords).
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
-                uint32_t* zero_words, uint32_t n_zero, hipStream_t s);
-// The table kernel's counter block: word 0 the claim counter (a 256-B block,
-// so that an A/B form can keep more state beside it).
-constexpr uint32_t kTableCtrWords = 64;
+                hipStream_t s);
+// sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
+// translation unit), one group of 64 blocks per wave; SF_OK or the launch
+// error.
+int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, const uint64_t* d_offsets,
+                        const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests, int* d_status, uint32_t* weak,
+                        const uint32_t* order, hipStream_t stream);
 
 }  // namespace sfi

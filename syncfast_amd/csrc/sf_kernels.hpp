@@ -37,20 +37,7 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // raw buffer, gfx9 family
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // ---------------------------------------------------------- wave helpers
-// The lane index.  A build with SF_OPAQUE_LANE reads it through an asm
-// statement the compiler cannot move, so that nothing derived from it is
-// hoisted out of a loop around a whole group (the persistent form of the
-// explicit-list kernel, whose loop otherwise keeps both hash paths' lane
-// addresses live across the other path).
-__device__ __forceinline__ int lane_id() {
-#ifdef SF_OPAQUE_LANE
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-#else
-  return threadIdx.x & 63;
-#endif
-}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // A value identical in every lane, moved to SGPRs so that everything derived
 // from it (buffer resources, loop bounds) stays scalar.
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
@@ -114,6 +101,10 @@ struct WaveGeo {
   bool lds_ok;        // 16-B aligned pieces and span < 4 GiB
 };
 
+// Cache policy of the aligned path's LDS-DMA: nt, the input is streamed once
+// (+1.4 % in A/B, profiles/r01/tune_sched_nt.log).
+constexpr int kLoadAux = 2;
+
 // Issue the LDS-DMA fill of step `step` (bytes [step*TILE, step*TILE+TILE) of
 // every block) into the wave's tile.  The buffer resource starts at the step
 // and covers the rest of the span, so lanes past the span read zeros.
@@ -128,33 +119,9 @@ __device__ __forceinline__ void issue_step(const uint8_t* span_ptr, uint64_t spa
   const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
   __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
-#ifndef SF_PIPE
-#define SF_PIPE 0  // 1: split LDS-read wait / mid-step DMA issue (A/B variant)
-#endif
-#ifndef SF_LOAD_AUX
-#define SF_LOAD_AUX 2  // nt: the input is streamed once (+1.4% in A/B, profiles/r01/tune_sched_nt.log)
-#endif
 #pragma unroll
   for (int j = 0; j < TILE / 16; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
-}
-
-#ifndef SF_SCALAR_ISSUE
-#define SF_SCALAR_ISSUE 0  // 1: span base/length made uniform once, per-step resource math in SALU (A/B)
-#endif
-// The same DMA step with the span base and length already in SGPRs (hoisted
-// out of the step loop): the per-step resource arithmetic is scalar.
-template <int TILE>
-__device__ __forceinline__ void issue_step_s(uint64_t ptr_s, uint64_t span_s, uint32_t step, const uint32_t* voff,
-                                             uint4* wave_tile) {
-  const uint64_t toff = (uint64_t)step * TILE;
-  const uint64_t left = span_s > toff ? span_s - toff : 0;
-  const uint32_t nrec = left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left;
-  __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr_s + toff), (short)0, (int)nrec, (int)kRsrcWord3);
-#pragma unroll
-  for (int j = 0; j < TILE / 16; ++j)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0, kLoadAux);
 }
 
 // Hash the block (off, size) owned by this lane; all 64 lanes of the wave
@@ -196,57 +163,16 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
     const uint4* my = wave_tile + lane * PIECES;
     const uint8_t* span_ptr = data + geo.base;
 
-#if defined(SF_EXPERIMENT_SEQ)
-    // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_SEQ, 4 KiB
-    // blocks): the same DMA volume per step, but one contiguous 64*TILE-byte
-    // piece of the wave's span instead of TILE bytes of each of 64 blocks
-    // 4 KiB apart (wrong digests) -- isolates the cost of the strided pattern.
-#define SF_ISSUE(step)                                                                     \
-  do {                                                                                     \
-    uint32_t vs[PIECES];                                                                   \
-    for (int j = 0; j < PIECES; ++j) vs[j] = (step) * (uint32_t)TILE * 63u + j * 1024u + lane * 16u; \
-    issue_step<TILE>(span_ptr, geo.span, (step), vs, wave_tile);                           \
-  } while (0)
-#elif SF_SCALAR_ISSUE
-    const uint64_t ptr_s = uniform_u64(reinterpret_cast<uint64_t>(span_ptr));
-    const uint64_t span_s = uniform_u64(geo.span);
-#define SF_ISSUE(step) issue_step_s<TILE>(ptr_s, span_s, (step), voff, wave_tile)
-#else
-#define SF_ISSUE(step) issue_step<TILE>(span_ptr, geo.span, (step), voff, wave_tile)
-#endif
-    if (nsteps > 0) SF_ISSUE(0);
+    if (nsteps > 0) issue_step<TILE>(span_ptr, geo.span, 0, voff, wave_tile);
     for (uint32_t t = 0; t < nsteps; ++t) {
       uint4 raw[PIECES];
-#ifndef SF_EXPERIMENT_NOLOAD
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int k = 0; k < PIECES; ++k) raw[k] = my[k ^ g];
-#if SF_PIPE
-      // Variant: only chunk 0's reads are waited for here (hipcc inserts the
-      // counted lgkmcnt before their first use); the rest land during
-      // chunk 0's compression, and the next DMA is issued after it.
-#else
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t + 1 < nsteps) SF_ISSUE(t + 1);
-#endif
-#else
-      // Experiment build only (make variant EXTRA=-DSF_EXPERIMENT_NOLOAD):
-      // same VALU work on register data, no loads -- isolates compute cost.
-#pragma unroll
-      for (int k = 0; k < PIECES; ++k) raw[k] = make_uint4(rel ^ (t * 977u + k), t + k, rel + k, voff[k & 7]);
-#endif
+      if (t + 1 < nsteps) issue_step<TILE>(span_ptr, geo.span, t + 1, voff, wave_tile);
 #pragma unroll
       for (int ch = 0; ch < CH; ++ch) {
-#if SF_PIPE && !defined(SF_EXPERIMENT_NOLOAD)
-        if (ch == 1) {
-          __builtin_amdgcn_sched_barrier(0);  // keep chunk 1's uses (and their waits) after chunk 0
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: reads done before the DMA rewrites the tile
-          // unconditional (no branch in the loop body): past the last step
-          // the resource has num_records 0, every lane reads zeros, nobody
-          // reads the tile again.
-          SF_ISSUE(t + 1);
-        }
-#endif
         uint32_t w[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -271,7 +197,6 @@ __device__ __forceinline__ void hash_wave(const uint8_t* __restrict__ data, uint
         st.compress(w);
       }
     }
-#undef SF_ISSUE
     c_done = nsteps * CH;
   } else {
     if constexpr (HAS_PAD) {
@@ -444,12 +369,6 @@ sha1_fixed_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, u
                   uint8_t* __restrict__ digests, const PadSchedule pad, uint32_t* __restrict__ weak) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR
-#if defined(SF_PRIO_EXP) && SF_PRIO_EXP == 1
-  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);  // A/B only: static priority for half the workgroups
-#elif defined(SF_PRIO_EXP) && SF_PRIO_EXP == 2
-  if (blockIdx.x % 3 == 1) __builtin_amdgcn_s_setprio(1);
-  else if (blockIdx.x % 3 == 2) __builtin_amdgcn_s_setprio(2);
-#endif
   fixed_wave<TILE, WEAK>(data, len, bs, nblocks, digests, pad, weak, (uint64_t)blockIdx.x * kWavesPerWG + wid,
                          smem + wid * 64 * (TILE / 16));
 }
@@ -544,9 +463,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 }
 #endif
 
-#ifndef SF_CHAIN_PRIO
-#define SF_CHAIN_PRIO 3  // wave priority of the stream's chain waves (A/B: make variant EXTRA=-DSF_CHAIN_PRIO=0)
-#endif
+constexpr int kChainPrio = 3;  // wave priority of the stream's chain waves
 // A stream's chain job on the chain wave of a block launch (wave 0 of one
 // of the first workgroups, sha1_fixed_chained_kernel).  Its digest loads are
 // staged through the workgroup's LDS tile (unused by a chain wave
@@ -558,7 +475,7 @@ sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_
 // launch sequence, profiles/r03/c3/seq/seq_chain_lds.txt).  Data chunks
 // [lo, hi) of each lane's run; part 0/2 then the padding chunk(s).
 __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave, uint4* __restrict__ tile) {
-  __builtin_amdgcn_s_setprio(SF_CHAIN_PRIO);  // latency-bound chains issue first on a shared SIMD
+  __builtin_amdgcn_s_setprio(kChainPrio);  // latency-bound chains issue first on a shared SIMD
   const int lane = lane_id();
   const uint32_t f = wave * 64 + lane;
   const bool valid = f < j.files;
@@ -626,89 +543,6 @@ __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave, uint
 // sha1_fixed_chained_kernel (a stream's batches with their chains) is in
 // sf_stream.hip, its own translation unit.
 
-#if defined(SF_TUNING) && !defined(SF_STREAM_TU)
-// Tuning variant: TWO blocks per lane (wave = 128 consecutive blocks; lane l
-// owns blocks l and 64 + l), 64-B LDS steps (8 KiB tile per wave), the two
-// compressions round-interleaved.  Fixed tiling, bs % 64 == 0, 16-B aligned
-// data; anything else goes through the one-block kernel.
-__global__ void __launch_bounds__(kThreads)
-sha1_fixed2_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, uint64_t nblocks,
-                   uint8_t* __restrict__ digests, const PadSchedule pad) {
-  constexpr int TILE = 64, PIECES = 4;
-  __shared__ uint4 smem[kWavesPerWG * 128 * PIECES];
-  const int lane = lane_id();
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerWG + wid) * 128;
-  if (first >= nblocks) return;
-  uint4* tile = smem + wid * 128 * PIECES;
-  const uint64_t blkA = first + lane, blkB = first + 64 + lane;
-  const bool vA = blkA < nblocks, vB = blkB < nblocks;
-  const uint32_t sA = vA ? (uint32_t)(len - blkA * bs < bs ? len - blkA * bs : bs) : 0u;
-  const uint32_t sB = vB ? (uint32_t)(len - blkB * bs < bs ? len - blkB * bs : bs) : 0u;
-  const uint64_t base = first * bs;
-  const uint64_t nvalid = nblocks - first < 128 ? nblocks - first : 128;
-  const uint64_t span = len - base < nvalid * (uint64_t)bs ? len - base : nvalid * (uint64_t)bs;
-  const uint64_t lastb = first + nvalid - 1;
-  const uint32_t last_size = (uint32_t)(len - lastb * bs < bs ? len - lastb * bs : bs);
-  const uint32_t min_size = last_size < bs ? last_size : bs;
-  Sha1 A, B;
-  A.init();
-  B.init();
-  const uint32_t nsteps = min_size / 64u;
-  uint32_t voff[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int b = j * 16 + lane / 4;
-    const int k = (lane % 4) ^ ((b >> 2) & 3);
-    voff[j] = (uint32_t)b * bs + (uint32_t)k * 16u;
-  }
-  const int g = (lane >> 2) & 3;
-  const uint4* myA = tile + lane * PIECES;
-  const uint4* myB = tile + (64 + lane) * PIECES;
-  const uint8_t* span_ptr = data + base;
-  auto issue = [&](uint32_t step) {
-    const uint64_t toff = (uint64_t)step * TILE;
-    const uint64_t left = span > toff ? span - toff : 0;
-    const uint32_t nrec = __builtin_amdgcn_readfirstlane(left > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)left);
-    const uint64_t ptr = uniform_u64(reinterpret_cast<uint64_t>(span_ptr + toff));
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ptr), (short)0, (int)nrec, (int)kRsrcWord3);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(tile + j * 64), 16, voff[j], 0, 0, SF_LOAD_AUX);
-  };
-  if (nsteps > 0) issue(0);
-  for (uint32_t t = 0; t < nsteps; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint4 ra[4], rb[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { ra[k] = myA[k ^ g]; rb[k] = myB[k ^ g]; }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + 1 < nsteps) issue(t + 1);
-    uint32_t wa[16], wb[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      wa[4 * q] = bswap32(ra[q].x); wa[4 * q + 1] = bswap32(ra[q].y); wa[4 * q + 2] = bswap32(ra[q].z); wa[4 * q + 3] = bswap32(ra[q].w);
-      wb[4 * q] = bswap32(rb[q].x); wb[4 * q + 1] = bswap32(rb[q].y); wb[4 * q + 2] = bswap32(rb[q].z); wb[4 * q + 3] = bswap32(rb[q].w);
-    }
-    Sha1::compress2(A, wa, B, wb);
-  }
-  if (pad.bytes == min_size && min_size == bs) {
-    A.compress_uniform(pad.kw);
-    B.compress_uniform(pad.kw);
-  } else {
-    const uint32_t ncA = n_chunks(sA), ncB = n_chunks(sB);
-    const uint32_t mx = n_chunks(bs);
-    for (uint32_t c = nsteps; c < mx; ++c) {
-      if (vA && c < ncA) { uint32_t w[16]; build_tail_chunk(w, data + blkA * bs, sA, c, ncA); A.compress(w); }
-      if (vB && c < ncB) { uint32_t w[16]; build_tail_chunk(w, data + blkB * bs, sB, c, ncB); B.compress(w); }
-    }
-  }
-  if (vA) A.store(digests + blkA * 20);
-  if (vB) B.store(digests + blkB * 20);
-}
-#endif
-
 // Many equal-size files in ONE launch with their blocks_hash chains.
 // `rows` files of `cols` full-size blocks.  Workgroups [0, chain_wgs) are
 // chain workgroups: each wave owns 64 files and runs chain_wave over S
@@ -721,11 +555,9 @@ sha1_fixed2_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32_t bs, 
 // Deadlock-free by construction: only chain waves wait, and only on block
 // waves, which never wait; the bounded poll is a backstop.
 // rows*m must be a multiple of 64 (no wave straddles two stages).
-#ifndef SF_STAGED_WPE
-#define SF_STAGED_WPE 4  // min waves/SIMD of the staged kernel (A/B: make variant EXTRA=-DSF_STAGED_WPE=1)
-#endif
+constexpr int kStagedWavesPerSimd = 4;  // min waves/SIMD of the staged kernel
 template <int TILE>
-__global__ void __launch_bounds__(kThreads, SF_STAGED_WPE)
+__global__ void __launch_bounds__(kThreads, kStagedWavesPerSimd)
 sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
                    uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
                    uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
@@ -804,9 +636,7 @@ constexpr int kListPieces = 9;
 
 // Cache policy of the slot DMA: the default (0), not the aligned path's nt
 // (see above).
-#ifndef SF_LIST_LOAD_AUX
-#define SF_LIST_LOAD_AUX 0
-#endif
+constexpr int kListLoadAux = 0;
 template <int NP>
 __device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t span4, uint32_t step,
                                              const uint32_t (&voff)[NP], uint4* wave_tile) {
@@ -819,7 +649,7 @@ __device__ __forceinline__ void issue_pieces(const uint8_t* span_ptr, uint64_t s
 #pragma unroll
   for (int j = 0; j < NP; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(wave_tile + j * 64), 16, voff[j], 0, 0,
-                                             SF_LIST_LOAD_AUX);
+                                             kListLoadAux);
 }
 
 // Words of chunk c of a message of `size` bytes whose data words (already
@@ -929,21 +759,10 @@ __device__ __forceinline__ void hash_wave_list(const uint8_t* __restrict__ data,
   }
 }
 
-#ifndef SF_TABLE_LB
-#define SF_TABLE_LB 3  // waves/SIMD the register budget is sized for (A/B: make tablevariant TEXTRA=-DSF_TABLE_LB=2)
-#endif
-#ifndef SF_TABLE_WG
-#define SF_TABLE_WG 4  // waves per workgroup (A/B: 1, 2)
-#endif
-#ifndef SF_TABLE_SNAKE
-#define SF_TABLE_SNAKE 2  // bit r: wave round r takes its groups in reverse (0: none, A/B)
-#endif
-#ifndef SF_TABLE_ROUND
-#define SF_TABLE_ROUND 1024u  // waves per round: MI355X's SIMDs (256 CUs x 4)
-#endif
-#ifndef SF_TABLE_PERSIST
-#define SF_TABLE_PERSIST 0  // 1: persistent waves claiming groups; 2: + generation priority (A/B records)
-#endif
+constexpr int kTableWavesPerSimd = 3;  // waves/SIMD the explicit-list kernel's register budget is sized for
+constexpr int kTableWG = 4;             // its waves per workgroup
+constexpr uint32_t kTableRound = 1024u; // waves per dispatch round: MI355X's SIMDs (256 CUs x 4)
+constexpr uint32_t kTableReversedRounds = 2u;  // bit r: round r takes its groups in reverse (round 1 only)
 
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
 // Used for content-defined boundaries, the reference KAT boundaries, ragged
@@ -987,41 +806,16 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
   geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
                ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
-#ifndef SF_TABLE_PRIO
-#define SF_TABLE_PRIO 0  // 1: critical-path priority (round 3; A/B record since the round-1 pairing)
-#endif
-#if SF_TABLE_PRIO && !SF_TABLE_PERSIST
-  // Critical-path priority (round 3): a sorted group longer than the list's
-  // compressions per lane of 3 waves on 1024 SIMDs (len / 64 + nblocks: exact
-  // for a list that tiles the data once) issues at priority 2.  Off since the
-  // first round's pairing (SF_TABLE_SNAKE): with it the build without the
-  // priority ran the CDC-like list 0.6-1.2 % faster in two order-rotated
-  // sessions, the 4 KiB list the same (profiles/r04/s20, s21).
-  if (order && (uint64_t)geo.max_nch * (64ull * 3 * 1024) >= len / 64 + nblocks) __builtin_amdgcn_s_setprio(2);
-#endif
-#ifdef SF_WAVE_TRACE
-  // Diagnostic build only (make tablevariant TEXTRA=-DSF_WAVE_TRACE): each
-  // group's start / end (s_memrealtime, 100 MHz), where it ran (HW_ID,
-  // XCC_ID) and its length, into the trace buffer passed as `weak` (unused
-  // by the plain kernel); scripts/table_trace.py reads it.
-  uint64_t trace_t0 = 0;
-  if constexpr (!WEAK) {
-    if (weak) trace_t0 = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
 
   Sha1 st;
   Adler wk;
-#ifndef SF_LIST_ALIGNED_TOO
-#define SF_LIST_ALIGNED_TOO 0  // 1: every 16-B aligned wave takes the 144-B slot path too (A/B)
-#endif
   // The slot path also takes aligned waves whose blocks differ in size: the
   // aligned path stages only the wave's shortest block's chunks through LDS
   // and loads the rest per lane (a CDC-like list laid out 16-B aligned: 2772
   // GiB/s that way, 3045 through the slots; equal 8 KiB blocks: 3165 aligned,
   // 3138 at byte offsets through the slots; profiles/r03/cdcx/).
   const uint64_t lo16 = lo & ~15ull;
-  const bool list_path = !WEAK && (SF_LIST_ALIGNED_TOO || !geo.lds_ok || geo.min_size != geo.max_size) &&
+  const bool list_path = !WEAK && (!geo.lds_ok || geo.min_size != geo.max_size) &&
                          ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && hi - lo16 < 0xF0000000ull;
   if (list_path)
     hash_wave_list(data, off, size, valid, lo16, hi - lo16, tile, st);
@@ -1038,145 +832,74 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
       if constexpr (WEAK) weak[blk] = wk.fin();
     }
   }
-#ifdef SF_WAVE_TRACE
-  if constexpr (!WEAK) {
-    if (weak) {
-      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-      const uint32_t hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID, 32 bits
-      const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID, 4 bits
-      const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
-      if (lane == 0) {
-        uint32_t* t = weak + g * 8;
-        t[0] = (uint32_t)trace_t0;
-        t[1] = (uint32_t)(trace_t0 >> 32);
-        t[2] = (uint32_t)t1;
-        t[3] = (uint32_t)(t1 >> 32);
-        t[4] = hwid;
-        t[5] = xcc;
-        t[6] = geo.max_nch;
-        t[7] = (list_path ? 1u : 0u) | (nvalid << 8);
-      }
-    }
-  }
-#endif
 }
 
 // The explicit-list kernel: wave w of the grid hashes group w (one group of
-// 64 blocks per wave, SF_TABLE_WG waves per workgroup).  How the waves of a
+// 64 blocks per wave, kTableWG waves per workgroup).  How the waves of a
 // sorted list are scheduled decides its rate (DESIGN.md section 3.4, round
-// 4; scripts/table_trace.py records every wave's start, end and SIMD):
+// 4, where the per-wave traces and the persistent forms measured against it
+// are recorded):
 //   * the sequencer issues the OLDEST wave of a SIMD first, so a wave that
 //     starts first -- with the sort, one of the longest groups -- runs at
 //     nearly the rate it would alone (1.33 us per compression beside two
 //     other waves, the 4 KiB list's waves 2.9 us), and the younger waves
 //     fill its gaps: hardware dispatch in the sort's order already gives the
 //     longest groups the critical path;
-//   * persistent waves that claim groups from a counter (SF_TABLE_PERSIST=1,
-//     kept for the record) lose that: a wave's age is its launch, not its
-//     group's, so an old wave that keeps claiming groups starves a younger
-//     neighbour, whose group then ends last (2501 vs 3031 GiB/s);
+//   * persistent waves that claim groups from a counter lose that: a wave's
+//     age is its launch, not its group's, so an old wave that keeps claiming
+//     groups starves a younger neighbour, whose group then ends last;
 //   * what is left is the end of the launch, and most of it is set by the
 //     first round: waves w, w + 1024 and w + 2048 land on one SIMD, so in
 //     the sort's order the same SIMDs would start with every round's
-//     longest group.  Round 1 therefore takes its groups in reverse
-//     (SF_TABLE_SNAKE, below): SIMD work max/mean 1.07 -> 1.047, the
-//     CDC-like list 2 % faster.  Persistent waves with the claim's
-//     generation as priority (SF_TABLE_PERSIST=2; SF_OPAQUE_LANE keeps a
-//     3-wave build to 80 spilled bytes, all outside the step loops) balance
-//     the end but issue slower while busy.
-// next_group (SF_TABLE_PERSIST builds only): the claim counter.
+//     longest group.  Round 1 therefore takes its groups in reverse (below):
+//     SIMD work max/mean 1.07 -> 1.047, the CDC-like list 2 % faster.
+// next_group: unused (kept in the signature until the list kernel's next
+// form replaces it).
 template <int TILE, bool WEAK = false>
-__global__ void __launch_bounds__(64 * SF_TABLE_WG, SF_TABLE_LB)
+__global__ void __launch_bounds__(64 * kTableWG, kTableWavesPerSimd)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
                   int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
                   uint32_t* __restrict__ next_group) {
   constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
-  __shared__ uint4 smem[SF_TABLE_WG * kWaveTile];
-  const int wid = SF_TABLE_WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ uint4 smem[kTableWG * kWaveTile];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint4* tile = smem + wid * kWaveTile;
   const uint32_t ngroups = (uint32_t)((nblocks + 63) / 64);  // <= 2^25: the launcher splits at 2^31 blocks
-#if SF_TABLE_PERSIST
-  // every claim moves the counter on, so each wave exits once it passes ngroups
-  auto claim = [&]() -> uint32_t {
-    uint32_t k = 0;
-    if ((threadIdx.x & 63) == 0) k = __hip_atomic_fetch_add(next_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(k);
-  };
-  // a wave's first group is its launch index; later ones come from the
-  // counter (zeroed by the sort), numbered on from the launch
-  const uint32_t launched = gridDim.x * SF_TABLE_WG;
-  uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
-  while (g < ngroups) {  // one call site: the group body is inlined once
-#if SF_TABLE_PERSIST == 2
-    // groups issue in claim order, not in their waves' launch order: the
-    // claim's generation (g / waves launched) sets the wave's priority
-    const uint32_t gen = g / launched;
-    if (gen == 0) __builtin_amdgcn_s_setprio(3);
-    else if (gen == 1) __builtin_amdgcn_s_setprio(2);
-    else if (gen == 2) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#else
-    (void)launched;
-#endif
-    table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
-    if (!next_group) break;
-    g = launched + claim();
-  }
-#else
   (void)next_group;
-  uint32_t g = blockIdx.x * SF_TABLE_WG + wid;
-#if SF_TABLE_SNAKE
+  uint32_t g = blockIdx.x * kTableWG + wid;
   // The first rounds of waves land one per SIMD per round (wave w and
-  // w + SF_TABLE_ROUND on the same SIMD, traces of round 4), so in the
-  // sort's order SIMD i would start with groups i, R + i and 2R + i: the
-  // longest group of every round on the same SIMDs (first-round work per
-  // SIMD 589..967 compressions, mean 764, on the CDC-like list).  Round 1
-  // takes its groups in reverse, pairing the longest of round 0 with the
-  // shortest of round 1.  Bit r of SF_TABLE_SNAKE reverses round r.  R is
-  // MI355X's 1024 SIMDs at compile time: a runtime R moved this kernel's
-  // compiled form and cost the 4 KiB list 6 % (profiles/r04/s18/); on a
-  // device with fewer SIMDs the reversal is one harmless permutation.
+  // w + kTableRound on the same SIMD, traces of round 4), so in the sort's
+  // order SIMD i would start with groups i, R + i and 2R + i: the longest
+  // group of every round on the same SIMDs (first-round work per SIMD
+  // 589..967 compressions, mean 764, on the CDC-like list).  Round 1 takes
+  // its groups in reverse, pairing the longest of round 0 with the shortest
+  // of round 1.  R is MI355X's 1024 SIMDs at compile time: a runtime R moved
+  // this kernel's compiled form and cost the 4 KiB list 6 % (profiles/r04/s18/);
+  // on a device with fewer SIMDs (a CPX/QPX partition) the reversal is one
+  // harmless permutation of round 1 whose gain does not carry over.
   if (order) {
-    const uint32_t R = SF_TABLE_ROUND, r = g / R;
-    if (r < 8 && ((SF_TABLE_SNAKE >> r) & 1u) && (r + 1) * R <= ngroups) g = r * R + (R - 1u - g % R);
+    const uint32_t R = kTableRound, r = g / R;
+    if (r < 8 && ((kTableReversedRounds >> r) & 1u) && (r + 1) * R <= ngroups) g = r * R + (R - 1u - g % R);
   }
-#endif
   if (g < ngroups) table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
-#endif
 }
 
-// Sort keys of an explicit block list for sha1_table_kernel's `order` (the
-// rocprim form, kept for SF_CLASS_SORT=0 builds; every class width of the
-// SF_TABLE_CLASS_BITS knob takes the counting sort of sf_sort.hip): the
-// block's compression count on a log scale with `mbits` mantissa bits
-// (classes 6.25 % wide with 4 bits, exact below 16; the key is clamped to
-// kmax = 255, so every block of >= 2^16 compressions shares the top class),
-// and its index.  A class holds many blocks, so
-// a wave's 64 blocks (consecutive in the stable sort: list order within a
-// class) lie close together in memory; an exact-count key spreads them over
-// the whole buffer (every nch value is rare), and 64 lanes streaming from 64
-// far-apart places run memory-bound: 4 KiB blocks in a shuffled order hashed
-// at 1200 GiB/s against 2857 in order (scripts/ragged_probe.py).
+// The length class of a block for sha1_table_kernel's `order` (sf_sort.hip's
+// counting sort): the block's compression count on a log scale with `mbits`
+// mantissa bits (classes 6.25 % wide with 4 bits, exact below 16; the key is
+// clamped to kmax = 255, so every block of >= 2^16 compressions shares the top
+// class).  A class holds many blocks, so a wave's 64 blocks (consecutive in
+// the stable sort: list order within a class) lie close together in memory;
+// an exact-count key spreads them over the whole buffer (every nch value is
+// rare), and 64 lanes streaming from 64 far-apart places run memory-bound:
+// 4 KiB blocks in a shuffled order hashed at 1200 GiB/s against 2857 in order
+// (scripts/ragged_probe.py).
 __device__ __forceinline__ uint16_t length_class(uint32_t nch, uint32_t mbits) {
   if (nch < (1u << mbits)) return (uint16_t)nch;
   const uint32_t e = 31u - (uint32_t)__builtin_clz(nch);  // floor(log2), >= mbits
   return (uint16_t)((e << mbits) + ((nch >> (e - mbits)) & ((1u << mbits) - 1u)));  // < 32 << mbits
 }
-
-// kmax: the largest key the sort looks at (blocks of a larger class share
-// it): 255 with 4 mantissa bits, so one 8-bit radix pass sorts the list.
-#ifndef SF_STREAM_TU
-__global__ void __launch_bounds__(256)
-table_keys_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint16_t* __restrict__ keys,
-                  uint32_t* __restrict__ idx, uint32_t mbits, uint32_t kmax) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = length_class(n_chunks_wide(sizes[i]), mbits);
-  keys[i] = (uint16_t)(k < kmax ? k : kmax);
-  idx[i] = (uint32_t)i;
-}
-#endif
 
 // Wire emission of the signature table as the reference's FILE_BLOCK
 // messages (src/sync/ssh/proto.rs:162-166): "FILE_BLOCK\n" + 20 raw digest

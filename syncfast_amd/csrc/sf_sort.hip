@@ -19,10 +19,9 @@
 namespace sf {
 
 constexpr int kSortThreads = 256;
-#ifndef SF_SORT_ROUNDS
-#define SF_SORT_ROUNDS 4  // blocks per thread per tile: 1024-block tiles (8: scatter 9.8 -> 7.7 us on the 0.5 M-block CDC-like list, profiles/r04/s28)
-#endif
-constexpr int kSortRounds = SF_SORT_ROUNDS;
+// blocks per thread per tile: 1024-block tiles (2048: scatter 9.8 -> 7.7 us
+// at 1024 on the 0.5 M-block CDC-like list, profiles/r04/s28)
+constexpr int kSortRounds = 4;
 constexpr uint32_t kSortTile = kSortThreads * kSortRounds;  // blocks per tile
 constexpr uint32_t kSortBinsMax = 1024;                      // 8- to 10-bit class keys
 
@@ -77,11 +76,8 @@ class_hist_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mbits
 // 2. Per bin (one workgroup each): exclusive prefix over the tiles, in
 // place, and the bin's total.
 __global__ void __launch_bounds__(kSortThreads)
-class_scan_kernel(uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ totals,
-                  uint32_t* __restrict__ zero_words, uint32_t n_zero) {
+class_scan_kernel(uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t* __restrict__ totals) {
   __shared__ uint32_t wsum[kSortThreads / 64];
-  if (zero_words && blockIdx.x == 0)  // the table kernel's counters
-    for (uint32_t i = threadIdx.x; i < n_zero; i += kSortThreads) zero_words[i] = 0u;
   uint32_t* col = hist + (uint64_t)blockIdx.x * ntiles;
   uint32_t carry = 0;
   for (uint32_t t0 = 0; t0 < ntiles; t0 += kSortThreads) {
@@ -181,29 +177,27 @@ size_t class_order_workspace(uint64_t n, uint32_t kmax) {
 
 template <uint32_t BINS>
 static void class_order_launch(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, uint32_t* hist,
-                               uint32_t ntiles, uint32_t* d_order, uint32_t* zero_words, uint32_t n_zero,
-                               hipStream_t s) {
+                               uint32_t ntiles, uint32_t* d_order, hipStream_t s) {
   uint32_t* totals = hist + (uint64_t)ntiles * BINS;
   hipLaunchKernelGGL(sf::class_hist_kernel<BINS>, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
                      hist, ntiles);
-  hipLaunchKernelGGL(sf::class_scan_kernel, dim3(BINS), dim3(sf::kSortThreads), 0, s, hist, ntiles, totals, zero_words,
-                     n_zero);
+  hipLaunchKernelGGL(sf::class_scan_kernel, dim3(BINS), dim3(sf::kSortThreads), 0, s, hist, ntiles, totals);
   hipLaunchKernelGGL(sf::class_scatter_kernel<BINS>, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits,
                      kmax, hist, totals, ntiles, d_order);
 }
 
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
-                uint32_t* zero_words, uint32_t n_zero, hipStream_t s) {
+                hipStream_t s) {
   if (n == 0) return SF_OK;
   if (n > 0xFFFFFFFFull || kmax >= sf::kSortBinsMax) return SF_EINVAL;
   const uint32_t ntiles = (uint32_t)((n + sf::kSortTile - 1) / sf::kSortTile);
   uint32_t* hist = static_cast<uint32_t*>(d_ws);
   if (kmax < 256)
-    class_order_launch<256>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
+    class_order_launch<256>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, s);
   else if (kmax < 512)
-    class_order_launch<512>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
+    class_order_launch<512>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, s);
   else
-    class_order_launch<1024>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, zero_words, n_zero, s);
+    class_order_launch<1024>(d_sizes, n, mbits, kmax, hist, ntiles, d_order, s);
   return hip_err(hipGetLastError());
 }
 
@@ -218,7 +212,7 @@ extern "C" int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uin
   void* ws = nullptr;
   const uint32_t kmax = (16u << (mbits < 4 ? 4 : mbits)) - 1u;
   if (hipMallocAsync(&ws, sfi::class_order_workspace(n, kmax), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
-  const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, nullptr, 0, s);
+  const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, s);
   (void)hipFreeAsync(ws, s);
   return rc;
 }

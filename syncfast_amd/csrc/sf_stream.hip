@@ -13,10 +13,6 @@
 #include "sf_internal.hpp"
 #include "sf_kernels.hpp"
 
-#ifndef SF_CHAIN_PACK
-#define SF_CHAIN_PACK 0  // 1: chain waves four to a workgroup of their own (A/B)
-#endif
-
 namespace sf {
 
 // Equal-size many-file batches as a stream (BASELINE configs[2], batch after
@@ -42,21 +38,7 @@ sha1_fixed_chained_kernel(const uint8_t* __restrict__ data, uint64_t len, uint32
   const uint32_t C = j0.waves + j1.waves;  // chain waves
   const uint32_t g = blockIdx.x;
   uint64_t bw;
-#if SF_CHAIN_PACK
-  // A/B (round 4): chain waves packed four to a workgroup of their own, so
-  // no block wave shares a workgroup (and its lifetime) with a chain
-  const uint32_t CW = (C + kWavesPerWG - 1) / kWavesPerWG;
-  if (g < CW) {
-    const uint32_t cw = g * kWavesPerWG + wid;
-    if (cw < j0.waves) chain_job(j0, cw, smem + wid * 64 * (TILE / 16));
-    else if (cw < C) chain_job(j1, cw - j0.waves, smem + wid * 64 * (TILE / 16));
-    return;
-  }
-  bw = (uint64_t)(g - CW) * kWavesPerWG + wid;
-  if (false) {
-#else
   if (g < C) {
-#endif
     if (wid == 0) {
       if (g < j0.waves) chain_job(j0, g, smem);
       else chain_job(j1, g - j0.waves, smem);
@@ -82,12 +64,8 @@ int launch_chained(const uint8_t* data, uint64_t len, uint32_t bs, uint64_t nblo
   // grid: C mixed workgroups (1 chain wave + 3 block waves), then 4 block
   // waves per workgroup for the rest
   const uint64_t C = j0.waves + j1.waves;
-#if SF_CHAIN_PACK
-  const unsigned grid = (unsigned)(ceil_div(C, sf::kWavesPerWG) + ceil_div(bwaves, sf::kWavesPerWG));
-#else
   const uint64_t rest = bwaves > 3 * C ? bwaves - 3 * C : 0;
   const unsigned grid = (unsigned)(C + ceil_div(rest, sf::kWavesPerWG));
-#endif
   if (grid == 0) return SF_OK;
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<128>, dim3(grid), dim3(sf::kThreads), 0, stream, data, len, bs,
                      nblocks, digests, pad, j0, j1, wpf, wpp, poff);

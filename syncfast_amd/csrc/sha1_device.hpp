@@ -61,36 +61,6 @@ struct Sha1 {
     }
     h0 += a; h1 += b; h2 += c; h3 += d; h4 += e;
   }
-  // Two independent compressions, round-interleaved (explicit ILP for the
-  // two-blocks-per-lane kernel variant).
-  __device__ __forceinline__ static void compress2(Sha1& A, uint32_t (&wa)[16], Sha1& B, uint32_t (&wb)[16]) {
-    uint32_t a0 = A.h0, b0 = A.h1, c0 = A.h2, d0 = A.h3, e0 = A.h4;
-    uint32_t a1 = B.h0, b1 = B.h1, c1 = B.h2, d1 = B.h3, e1 = B.h4;
-#pragma unroll
-    for (int t = 0; t < 80; ++t) {
-      uint32_t wt0, wt1;
-      if (t < 16) {
-        wt0 = wa[t];
-        wt1 = wb[t];
-      } else {
-        wt0 = rotl(xor3(wa[(t + 13) & 15], wa[(t + 8) & 15], wa[(t + 2) & 15]) ^ wa[t & 15], 1);
-        wt1 = rotl(xor3(wb[(t + 13) & 15], wb[(t + 8) & 15], wb[(t + 2) & 15]) ^ wb[t & 15], 1);
-        wa[t & 15] = wt0;
-        wb[t & 15] = wt1;
-      }
-      uint32_t f0, f1, k;
-      if (t < 20) { f0 = ch(b0, c0, d0); f1 = ch(b1, c1, d1); k = 0x5A827999u; }
-      else if (t < 40) { f0 = xor3(b0, c0, d0); f1 = xor3(b1, c1, d1); k = 0x6ED9EBA1u; }
-      else if (t < 60) { f0 = maj(b0, c0, d0); f1 = maj(b1, c1, d1); k = 0x8F1BBCDCu; }
-      else { f0 = xor3(b0, c0, d0); f1 = xor3(b1, c1, d1); k = 0xCA62C1D6u; }
-      const uint32_t t0 = rotl(a0, 5) + f0 + e0 + k + wt0;
-      const uint32_t t1 = rotl(a1, 5) + f1 + e1 + k + wt1;
-      e0 = d0; d0 = c0; c0 = rotl(b0, 30); b0 = a0; a0 = t0;
-      e1 = d1; d1 = c1; c1 = rotl(b1, 30); b1 = a1; a1 = t1;
-    }
-    A.h0 += a0; A.h1 += b0; A.h2 += c0; A.h3 += d0; A.h4 += e0;
-    B.h0 += a1; B.h1 += b1; B.h2 += c1; B.h3 += d1; B.h4 += e1;
-  }
   // Compression of a chunk whose message words are the same for every lane
   // (the padding-only chunk ending a message of a 64-B multiple length).
   // kw[t] = K_t + W_t is precomputed on the host and arrives as kernel

@@ -39,23 +39,35 @@ def test_every_include_header_is_checked():
     assert sorted(os.listdir(os.path.join(ROOT, "include"))) == ["syncfast_amd.h", "syncfast_amd_test.h"]
 
 
-def _strip_tuning_blocks(src):
-    """Source text without the #ifdef SF_TUNING ... #endif regions (tuning
-    builds only; the shipped library is built without SF_TUNING)."""
-    out, depth = [], 0
-    for line in src.splitlines():
-        t = line.strip()
-        if depth:
-            if t.startswith("#if"):
-                depth += 1
-            elif t.startswith("#endif"):
-                depth -= 1
-            continue
-        if t.startswith("#ifdef SF_TUNING") or t.startswith("#if defined(SF_TUNING)"):
-            depth = 1
-            continue
-        out.append(line)
-    return "\n".join(out)
+# A/B forms retired from the product sources in round 5:
+# they live in git history and DESIGN.md's records, not in the shipped code.
+RETIRED_MACROS = ("SF_EXPERIMENT_SEQ", "SF_EXPERIMENT_NOLOAD", "SF_PIPE", "SF_SCALAR_ISSUE", "SF_PRIO_EXP",
+                  "SF_TUNING", "SF_VARIANT", "SF_STAGED_EXP", "SF_TABLE_PRIO", "SF_TABLE_PERSIST", "SF_TABLE_WPS",
+                  "SF_OPAQUE_LANE", "SF_LIST_ALIGNED_TOO", "SF_CHAIN_PACK", "SF_WAVE_TRACE", "SF_CLASS_SORT",
+                  "SF_CLASS_BITS_FORCE", "SF_NO_CHAIN_HELPER", "SF_FIXED_WPE", "SF_STAGED_WPE", "SF_TABLE_SNAKE",
+                  "SF_TABLE_LB", "SF_TABLE_WG", "SF_TABLE_ROUND", "SF_CHAIN_DEPTH", "SF_SORT_ROUNDS", "SF_LOAD_AUX",
+                  "SF_LIST_LOAD_AUX", "SF_CHAIN_PRIO")
+# The only preprocessor conditionals the product sources may hold: the
+# translation-unit switch of the shared kernel header, the host compiler's
+# HIP platform define and the host SHA-NI path.
+ALLOWED_CONDITIONALS = ("SF_STREAM_TU", "__HIP_PLATFORM_AMD__", "__x86_64__", "SF_WIRE_CHUNK_DEFAULT")
+
+
+def _product_sources():
+    csrc = os.path.join(ROOT, "syncfast_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)):
+        if fn.endswith((".hip", ".hpp", ".cpp", ".h")) or fn == "Makefile":
+            yield fn, open(os.path.join(csrc, fn)).read()
+
+
+def test_product_kernels_carry_no_retired_ab_forms():
+    for fn, src in _product_sources():
+        for m in RETIRED_MACROS:
+            assert not re.search(r"\b%s\b" % m, src), (fn, m)
+        for line in src.splitlines():
+            t = line.strip()
+            if re.match(r"#\s*(if|ifdef|ifndef|elif)\b", t):
+                assert any(a in t for a in ALLOWED_CONDITIONALS), (fn, t)
 
 
 def test_environment_read_only_at_load():
@@ -65,7 +77,7 @@ def test_environment_read_only_at_load():
     csrc = os.path.join(ROOT, "syncfast_amd", "csrc")
     for fn in sorted(os.listdir(csrc)):
         if fn.endswith((".hip", ".hpp", ".cpp", ".h")) and fn != "sf_knobs.cpp":
-            src = _strip_tuning_blocks(open(os.path.join(csrc, fn)).read())
+            src = open(os.path.join(csrc, fn)).read()
             assert "getenv" not in src, fn
 
 

@@ -164,7 +164,7 @@ def test_default_sort_large_cdc_list(gpu, knobs):
 @pytest.mark.parametrize("nblocks", [64 * 2047, 64 * 2048 - 1, 64 * 2048, 64 * 2048 + 1, 64 * 3072 + 5])
 def test_sorted_round_reversal_edges(gpu, knobs, nblocks):
     # wave round 1 (groups 1024..2047 of the sorted order) takes its groups
-    # in reverse when the launch holds it whole (SF_TABLE_SNAKE): lists just
+    # in reverse when the launch holds it whole (kTableReversedRounds): lists just
     # below, at and above 2048 groups, small blocks of every class, every
     # digest at its own index = the oracle
     knobs.set("SF_TEST_TABLE_SORT", 1)
