@@ -363,6 +363,38 @@ int sf_index_files(const char *const *paths, uint32_t n_files, uint32_t block_si
                    sf_block_sig *out, uint64_t cap, uint64_t *first_row, uint8_t *blocks_hashes,
                    uint64_t *n_out, uint32_t *bad_file);
 
+/* Many files in the reference's default mode: what index_path
+ * (src/index.rs:685-715) does with one index_file (src/index.rs:610-659) per
+ * file, each file cut by the caller's chunker (cdchunking's ZPAQ,
+ * src/index.rs:622-625) on its own open descriptor, as ONE pipeline.  File f
+ * is the regular file open on fds[f]; stamps[f] (stamps may be NULL) its
+ * sf_file_stamp_fd taken before the chunker read it; its list is block i =
+ * [offsets[f][i], offsets[f][i] + sizes[f][i]) for i < n_blocks[f],
+ * offset-ordered (a chunker's output).  The files are read again with pread
+ * only (the descriptors' positions are not used or moved), by windows packed
+ * into pinned stages of about stage_bytes (0 = 256 MiB; a window of one
+ * larger block is a stage of its own) by a pool of reader threads; per stage
+ * one H2D copy, one length-class sort + one explicit-list kernel launch over
+ * every block of every file in it, one D2H, overlapped with the reading of
+ * the next stage.  out: file 0's rows, then file 1's, ... (offsets relative
+ * to each file); first_row (n_files + 1 entries): where each file's rows
+ * start (written first, from n_blocks); blocks_hashes: 20 B per file,
+ * compute_blocks_hash (src/index.rs:661-682) over its digests in list order
+ * (SHA1("") for a file with no blocks).  SF_ENOSPC (nothing read) when cap <
+ * first_row[n_files].  Each file succeeds or fails alone: file_status (may be
+ * NULL, n_files entries) receives SF_OK or, for that file, SF_EAGAIN (its
+ * stamp differs from stamps[f] at the call, or moved before its last window
+ * was read: cut it again), SF_ERANGE / SF_EINVAL (its list: past the end of
+ * the file / offsets going backwards), SF_EINVAL (fds[f] is not an open
+ * regular file), SF_EIO (fstat or a read failed); a failed file's rows are not
+ * valid and its blocks_hash is zeroed, every other file's are complete.  The
+ * call returns SF_OK, or the first failing file's code with *bad_file (may be
+ * NULL) = its index; a device error fails the whole call.  Blocking. */
+int sf_index_fds_blocks(const int *fds, const sf_file_stamp *stamps, uint32_t n_files,
+                        const uint64_t *const *offsets, const uint32_t *const *sizes, const uint64_t *n_blocks,
+                        uint64_t stage_bytes, sf_block_sig *out, uint64_t cap, uint64_t *first_row,
+                        uint8_t *blocks_hashes, int *file_status, uint32_t *bad_file);
+
 /* compute_blocks_hash (src/index.rs:661-682) on the host: SHA-1 over the
  * n 20-byte digests in order.  Sequential by definition; runs on a host
  * core (SHA-NI when the CPU has it). */

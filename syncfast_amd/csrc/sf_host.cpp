@@ -865,6 +865,10 @@ int index_list_pipeline(FillFn fill, const uint64_t* offsets, const uint32_t* si
 // the call starts -- against the caller's, taken before its chunker read the
 // file -- and after the last window is read: a file changed in between gives
 // SF_EAGAIN, never rows that mix one version's boundaries with another's bytes.
+}  // namespace
+
+namespace sfi {
+
 bool stamp_of(int fd, sf_file_stamp* s, mode_t* mode) {
   struct stat sb;
   if (fstat(fd, &sb) != 0) return false;
@@ -888,6 +892,10 @@ bool same_stamp(const sf_file_stamp& a, const sf_file_stamp& b) {
          a.mtime_nsec == b.mtime_nsec &&
          (a.nlink != b.nlink || (a.ctime_sec == b.ctime_sec && a.ctime_nsec == b.ctime_nsec));
 }
+
+}  // namespace sfi
+
+namespace {
 
 // body(stamp, mode) between two stamps of fd.  A read that came up short (the
 // file shrank: SF_EIO) or a complete one over a file whose stamp moved is

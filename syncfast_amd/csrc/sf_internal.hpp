@@ -15,6 +15,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <sys/types.h>
 
 #include <algorithm>
 #include <atomic>
@@ -254,6 +255,12 @@ class HostLease {
   HostRes* own_ = nullptr;
   std::vector<void*> tmp_dev_, tmp_pin_;
 };
+
+// fstat(fd) as a stamp (and the file's mode); false if fstat fails.  Two
+// stamps match when dev, ino, size and mtime are equal and, unless the link
+// count changed, ctime too (include/syncfast_amd.h, sf_file_stamp).
+bool stamp_of(int fd, sf_file_stamp* s, mode_t* mode);
+bool same_stamp(const sf_file_stamp& a, const sf_file_stamp& b);
 
 // Reader threads of the pread routes (sf_index_file, sf_index_files).
 // SF_IO_THREADS overrides the default of 16 (A/B knob, latched at load).  With the stat phase

@@ -214,6 +214,53 @@ def index_files(paths: Sequence, block_size: int, stage_bytes: int = 0) -> Tuple
         return out[:need.value], first, hashes[:n]
 
 
+def index_fds_blocks(fds: Sequence[int], lists: Sequence[Tuple[object, object]], stamps: Sequence = None,
+                     stage_bytes: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+    """Many files in the reference's default mode through one pipeline
+    (sf_index_fds_blocks): file k is the regular file open on fds[k], cut by
+    the caller's chunker into lists[k] = (offsets, sizes); stamps[k]
+    (file_stamp before chunking, or None for all) is checked when the call
+    starts and after the file's last window is read.
+
+    Returns (rows, first_row, blocks_hashes, status): file k's rows are
+    rows[first_row[k]:first_row[k+1]], its blocks_hash blocks_hashes[k], and
+    status[k] its own result (SF_OK, or SF_EAGAIN / SF_ERANGE / SF_EINVAL /
+    SF_EIO for that file alone: its rows are not valid, it must be cut
+    again).  A per-file failure does not raise; a call-level one (device,
+    arguments) does."""
+    n = len(fds)
+    if len(lists) != n or (stamps is not None and len(stamps) != n):
+        raise ValueError("fds, lists and stamps differ in length")
+    offs, szs = [], []
+    for o, z in lists:
+        o = np.ascontiguousarray(o, dtype=np.uint64).reshape(-1)
+        z = np.ascontiguousarray(z, dtype=np.uint32).reshape(-1)
+        if o.size != z.size:
+            raise ValueError("offsets and sizes differ in length")
+        offs.append(o)
+        szs.append(z)
+    nb = np.array([o.size for o in offs] or [0], np.uint64)
+    po = (ctypes.c_void_p * max(n, 1))(*[o.ctypes.data if o.size else None for o in offs])
+    pz = (ctypes.c_void_p * max(n, 1))(*[z.ctypes.data if z.size else None for z in szs])
+    fda = np.array(list(fds) or [0], np.int32)
+    st = None
+    if stamps is not None:
+        st = (FileStamp * max(n, 1))(*stamps)
+    total = int(nb[:n].sum()) if n else 0
+    out = np.zeros(max(total, 1), SIG_DTYPE)
+    first = np.zeros(n + 1, np.uint64)
+    hashes = np.zeros((max(n, 1), 20), np.uint8)
+    status = np.zeros(max(n, 1), np.int32)
+    bad = ctypes.c_uint32(0)
+    rc = lib().sf_index_fds_blocks(fda.ctypes.data, st, n, po, pz, nb.ctypes.data, stage_bytes,
+                                   out.ctypes.data_as(ctypes.POINTER(BlockSig)), total,
+                                   first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), hashes.ctypes.data,
+                                   status.ctypes.data, ctypes.byref(bad))
+    if rc != 0 and not (n and bad.value < n and status[bad.value] == rc):
+        check(rc, "sf_index_fds_blocks")
+    return out[:total], first, hashes[:n], status[:n]
+
+
 def blocks_hash(digests) -> bytes:
     """compute_blocks_hash: SHA-1 over the 20-byte digests in order."""
     d = _u8(digests)

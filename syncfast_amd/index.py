@@ -474,25 +474,34 @@ class Index:
         sf_index_buffer_blocks.  The descriptor routes compare the file's
         stamp (fstat, taken before the chunker read it) when they start and
         after their last read: a file written while it is indexed is indexed
-        again from a new open (at most CHANGED_RETRIES times, then the
-        SF_EAGAIN error propagates), never stored as rows that mix two
-        versions of it."""
+        again from a new open, never stored as rows that mix two versions of
+        it.  A file that keeps changing (a log being appended to) is, after
+        CHANGED_RETRIES attempts, indexed in ONE pass as the reference does
+        (src/index.rs:615-647): its bytes are read once from one open, the
+        chunker cuts those bytes and the same bytes are hashed
+        (sf_index_buffer_blocks / sf_index_buffer), so the rows describe the
+        bytes read whatever the writer does meanwhile.  (Stamps are only as
+        fine as the filesystem's clock tick: a same-size write within the
+        tick of the stamp is not seen, include/syncfast_amd.h.)"""
         self._need_chunker()
         for attempt in range(CHANGED_RETRIES):
             try:
                 self._index_file_once(path, name, force=attempt > 0)
                 return
             except SfError as e:
-                if e.code != SF_EAGAIN or attempt + 1 == CHANGED_RETRIES:
+                if e.code != SF_EAGAIN:
                     raise
                 log.info("File %s changed while it was indexed, indexing it again", path)
+        log.info("File %s keeps changing: indexing the bytes of one read", path)
+        self._index_file_once(path, name, force=True, one_pass=True)
 
-    def _index_file_once(self, path, name, force: bool) -> None:
+    def _index_file_once(self, path, name, force: bool, one_pass: bool = False) -> None:
         ch = self.chunker
         native = None  # (rows, blocks_hash) from a native route
         with open(path, "rb") as f:  # File::open first: same error on a missing file
             seekable = _seekable(f)
-            stamp = host.file_stamp(f.fileno()) if seekable and (isinstance(ch, FixedChunker) or ch.stream) else None
+            stamp = host.file_stamp(f.fileno()) if seekable and not one_pass and \
+                (isinstance(ch, FixedChunker) or ch.stream) else None
             mtime = DateTimeUtc.from_ns(stamp.mtime_sec * 10**9 + stamp.mtime_nsec) if stamp else _mtime(f)
             file_id, up_to_date = self.add_file(name, mtime)
             if up_to_date:
@@ -502,11 +511,15 @@ class Index:
                 # restored it, or only the ctime changed): index it anyway
                 self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (file_id,))
             if isinstance(ch, FixedChunker):
-                if seekable:
+                if one_pass:  # the bytes of one read, hashed from host memory
+                    raw = f.read()
+                    rows_np = host.index_buffer(raw, ch.block_size)
+                    native = (rows_np, host.blocks_hash(np.ascontiguousarray(rows_np["sha1"])))
+                elif seekable:
                     native = host.index_fd_fixed(f.fileno(), ch.block_size, stamp)
                 else:  # a FIFO: read sequentially from this open, as File::open + read do
                     native = host.index_fd(f.fileno(), ch.block_size)
-            elif ch.stream and seekable:
+            elif ch.stream and seekable and not one_pass:
                 sizes = [int(x) for x in ch.fn(f)]
                 if sum(sizes) != stamp.size and _stamp_moved(f.fileno(), stamp):
                     raise SfError(SF_EAGAIN, f"index_file({os.fsdecode(path)})")  # written while chunked
@@ -539,7 +552,7 @@ class Index:
         self.db.executemany("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);",
                             ((hx[40 * i:40 * i + 40], file_id, offs[i], sizes[i]) for i in range(b - a)))
 
-    def index_path(self, path, batch_bytes: int = 256 << 20) -> None:
+    def index_path(self, path, batch_bytes: int = 256 << 20, chunk_threads: int = 0) -> None:
         """Index files and directories recursively (src/index.rs:685-715).
 
         Same walk, names and mtime gate as the reference.  With a
@@ -547,7 +560,15 @@ class Index:
         native pipeline (sf_index_files) in stages of `batch_bytes`: pinned
         host buffers filled by a pread thread pool, one H2D copy and one
         device launch per stage (blocks + every file's blocks_hash), reading
-        overlapped with the device.  batch_bytes=0 indexes file by file."""
+        overlapped with the device.  With BoundaryChunker(stream=True) -- the
+        reference's default mode -- the chunker cuts the files on a pool of
+        `chunk_threads` threads (0: one per core, at most 16; a chunker is
+        per-file state, so files cut independently), and every batch of about
+        `batch_bytes` of cut files goes through ONE native pipeline
+        (sf_index_fds_blocks: the open descriptors re-read by windows into
+        packed pinned stages, one sort + one explicit-list launch per stage)
+        while the pool cuts the next batch.  batch_bytes=0 indexes file by
+        file."""
         self._need_chunker()
         todo: List[Tuple[Path, PurePath]] = []
         self._index_path_rec(Path(path), PurePath(""), todo)
@@ -558,9 +579,8 @@ class Index:
                 self.index_file(p, rel)
             return
         if isinstance(self.chunker, BoundaryChunker):
-            if self.chunker.stream:  # file by file: chunker over the open file, the library re-reads it
-                for p, rel in todo:
-                    self.index_file(p, rel)
+            if self.chunker.stream:
+                self._index_batched_fds(todo, batch_bytes, chunk_threads)
             else:
                 self._index_batched_boundaries(todo, batch_bytes)
             return
@@ -609,6 +629,108 @@ class Index:
         for k, (file_id, _p) in enumerate(pending):
             self._insert_rows(file_id, rows, int(first[k]), int(first[k + 1]))
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
+
+    def _index_batched_fds(self, todo, batch_bytes: int, chunk_threads: int) -> None:
+        """The default (content-defined) mode over many files, the files cut
+        in parallel and hashed as ONE pipeline per batch.
+
+        Each file is opened once and stamped (sf_file_stamp_fd: its mtime is
+        the one stored, the mtime gate runs in walk order, so file_ids are the
+        reference's); the chunker streams the open file on a pool thread; a
+        batch of about `batch_bytes` of cut files (and at most a quarter of
+        the descriptor limit) goes to sf_index_fds_blocks on those same
+        descriptors while the pool cuts the next batch.  A file written while
+        it was cut or read (SF_EAGAIN for it alone) is indexed again through
+        index_file, in its place, so rows stay in walk order; a FIFO in the
+        tree is indexed through index_file from its own open."""
+        import resource
+        from concurrent.futures import ThreadPoolExecutor
+
+        ch = self.chunker
+        threads = chunk_threads if chunk_threads > 0 else min(16, os.cpu_count() or 1)
+        soft = resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+        max_files = max(16, min(4096, (soft if soft > 0 else 1024) // 4))
+
+        def cut(f, stamp):
+            sizes = [int(x) for x in ch.fn(f)]
+            if sum(sizes) != stamp.size and _stamp_moved(f.fileno(), stamp):
+                return None  # written while it was cut
+            return _sizes_ok(sizes, stamp.size)
+
+        def finish(batch, futs):
+            try:
+                cuts = [fu.result() for fu in futs]
+                keep = [k for k, c in enumerate(cuts) if c is not None]
+                lists = [(_offsets(cuts[k]), np.asarray(cuts[k], np.uint32)) for k in keep]
+                res = host.index_fds_blocks([batch[k][3].fileno() for k in keep], lists,
+                                            [batch[k][4] for k in keep], stage_bytes=batch_bytes) if keep else None
+            finally:
+                for _fid, _p, _rel, f, _st in batch:
+                    f.close()
+            pos = {k: j for j, k in enumerate(keep)}
+            for k, (fid, p, rel, _f, _st) in enumerate(batch):
+                j = pos.get(k)
+                if j is not None and res[3][j] == 0:
+                    rows, first, hashes, _status = res
+                    self._insert_rows(fid, rows, int(first[j]), int(first[j + 1]))
+                    self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;",
+                                    (bytes(hashes[j]).hex(), fid))
+                    continue
+                code = SF_EAGAIN if j is None else int(res[3][j])
+                if code != SF_EAGAIN:
+                    raise SfError(code, f"index_file({os.fsdecode(p)})")
+                log.info("File %s changed while it was indexed, indexing it again", p)
+                self.db.execute("DELETE FROM blocks WHERE file_id = ?;", (fid,))
+                self._index_file_changed(p, rel)
+
+        prev = None
+        batch, futs, nbytes = [], [], 0
+        pool = ThreadPoolExecutor(max_workers=threads)
+        try:
+            for p, rel in todo:
+                f = open(p, "rb")  # File::open first: same error on a missing file
+                try:
+                    if not _seekable(f):  # a FIFO: read from its own open, sequentially
+                        f.close()
+                        self.index_file(p, rel)
+                        continue
+                    stamp = host.file_stamp(f.fileno())
+                    file_id, up_to_date = self.add_file(
+                        rel, DateTimeUtc.from_ns(stamp.mtime_sec * 10**9 + stamp.mtime_nsec))
+                except BaseException:
+                    f.close()
+                    raise
+                if up_to_date:
+                    f.close()
+                    continue
+                batch.append((file_id, p, rel, f, stamp))
+                futs.append(pool.submit(cut, f, stamp))
+                nbytes += stamp.size
+                if nbytes >= batch_bytes or len(batch) >= max_files:
+                    if prev is not None:
+                        finish(*prev)  # hashed while the pool cuts this batch
+                    prev, batch, futs, nbytes = (batch, futs), [], [], 0
+            if prev is not None:
+                finish(*prev)
+            if batch:
+                finish(batch, futs)
+        finally:
+            pool.shutdown(wait=True)  # no chunker still reading a descriptor closed below
+            for b in ([prev[0]] if prev is not None else []) + [batch]:
+                for _fid, _p, _rel, f, _st in b:
+                    f.close()  # idempotent: the finished batches' are closed already
+
+    def _index_file_changed(self, path, name) -> None:
+        """index_file of a file whose first pass saw it change: its row was
+        added in walk order already, so only its blocks are indexed again."""
+        for attempt in range(CHANGED_RETRIES):
+            try:
+                self._index_file_once(path, name, force=True)
+                return
+            except SfError as e:
+                if e.code != SF_EAGAIN:
+                    raise
+        self._index_file_once(path, name, force=True, one_pass=True)
 
     def _index_batched_boundaries(self, todo, batch_bytes: int) -> None:
         """The default (content-defined) mode over many files: each file is

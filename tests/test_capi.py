@@ -469,3 +469,59 @@ def test_chained_kernel_is_the_measured_one():
     assert kernel_code_sha256(symbol=CHAINED_KERNEL) == rec["kernel_code_sha256"], \
         "the chained kernel changed: re-measure with scripts/c3_seq.sh and update the record"
 
+
+
+def test_fds_blocks_checks_before_any_device_call(tmp_path):
+    """sf_index_fds_blocks: the plan (first_row), SF_ENOSPC and each file's
+    own checks (stale stamp, a list past the end or going backwards, a pipe)
+    come before any device work; files with no blocks get SHA1("") -- so all
+    of this runs without a GPU."""
+    import time
+    paths = []
+    for k, n in enumerate([0, 100, 200, 0]):
+        p = tmp_path / f"f{k}"
+        p.write_bytes(bytes(range(256))[:n] if n <= 256 else b"")
+        paths.append(p)
+    fs = [open(p, "rb") for p in paths]
+    r, w = os.pipe()
+    try:
+        stamps = [host.file_stamp(f.fileno()) for f in fs]
+        time.sleep(0.02)
+        with open(paths[1], "r+b") as g:
+            g.write(b"\x00")
+        lists = [([], []), ([0, 50], [50, 50]), ([0, 100, 50], [100, 50, 50]), ([], [])]
+        rows, first, hashes, status = host.index_fds_blocks([f.fileno() for f in fs], lists, stamps)
+        assert list(first) == [0, 0, 2, 5, 5]
+        assert list(status) == [0, _lib.SF_EAGAIN, _lib.SF_EINVAL, 0]
+        assert bytes(hashes[0]).hex() == bytes(hashes[3]).hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"
+        assert bytes(hashes[1]) == bytes(20) and bytes(hashes[2]) == bytes(20)
+        # past the end; a pipe
+        rows, first, hashes, status = host.index_fds_blocks([fs[2].fileno(), r], [([150], [51]), ([0], [1])])
+        assert list(status) == [_lib.SF_ERANGE, _lib.SF_EINVAL]
+        # capacity and arguments: call-level errors
+        L = syncfast_amd.lib()
+        first = np.zeros(2, np.uint64)
+        nb = np.array([2], np.uint64)
+        o = np.array([0, 50], np.uint64)
+        s = np.array([50, 50], np.uint32)
+        po = (ctypes.c_void_p * 1)(o.ctypes.data)
+        pz = (ctypes.c_void_p * 1)(s.ctypes.data)
+        fd = np.array([fs[2].fileno()], np.int32)
+        hh = np.zeros(20, np.uint8)
+        out = np.zeros(2, host.SIG_DTYPE)
+        sig = out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig))
+        u64p = first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        assert L.sf_index_fds_blocks(fd.ctypes.data, None, 1, po, pz, nb.ctypes.data, 0, sig, 1, u64p,
+                                     hh.ctypes.data, None, None) == _lib.SF_ENOSPC
+        assert list(first) == [0, 2]
+        assert L.sf_index_fds_blocks(None, None, 1, po, pz, nb.ctypes.data, 0, sig, 2, u64p, hh.ctypes.data,
+                                     None, None) == _lib.SF_EINVAL
+        assert L.sf_index_fds_blocks(fd.ctypes.data, None, 1, po, pz, nb.ctypes.data, 0, None, 2, u64p,
+                                     hh.ctypes.data, None, None) == _lib.SF_EINVAL
+        assert L.sf_index_fds_blocks(None, None, 0, None, None, None, 0, None, 0, None, None, None,
+                                     None) == _lib.SF_OK
+    finally:
+        for f in fs:
+            f.close()
+        os.close(r)
+        os.close(w)

@@ -236,3 +236,40 @@ def test_index_file_retries_a_file_written_while_indexed(gpu, tmp_path, small_st
     dig, wbh = _want(now, offs, sizes)
     assert [h.bytes for h, _o, _s in rows] == [bytes(d) for d in dig]
     assert bh.bytes == wbh and int(sizes.sum()) == len(now)
+
+
+@pytest.mark.parametrize("mode", ["boundary", "fixed"])
+def test_index_file_of_a_file_appended_on_every_window(gpu, tmp_path, small_stages, mode):
+    """a file appended to after every window the library reads (a
+    log) never gets through the descriptor routes; after CHANGED_RETRIES
+    attempts index_file indexes the bytes of one read (the reference's single
+    pass, src/index.rs:615-647) instead of failing the walk."""
+    p = tmp_path / "log"
+    p.write_bytes(oracle.splitmix_bytes(3 * MIB + 5, 6160).tobytes())
+    seen = []
+
+    def hook(window):
+        seen.append(window)
+        with open(p, "ab") as g:
+            g.write(b"another line\n")
+
+    def chunk(f):
+        return _cdc_like_sizes(len(f.read()), 6161).tolist()
+
+    ch = BoundaryChunker(chunk, stream=True) if mode == "boundary" else FixedChunker(4096)
+    idx = Index.open_in_memory(chunker=ch)
+    _lib.set_read_hook(hook)
+    try:
+        idx.index_file(p, "log")
+    finally:
+        _lib.set_read_hook(None)
+    assert len(seen) >= 3
+    fid, _m, bh = idx.get_file("log")
+    rows = idx.list_file_blocks(fid)
+    total = sum(s for _h, _o, s in rows)
+    data = p.read_bytes()[:total]  # the bytes of the one read; the log grew only at its end since
+    offs = np.asarray([o for _h, o, _s in rows], np.uint64)
+    sizes = np.asarray([s for _h, _o, s in rows], np.uint32)
+    dig, wbh = _want(data, offs, sizes)
+    assert [h.bytes for h, _o, _s in rows] == [bytes(d) for d in dig]
+    assert bh.bytes == wbh and total >= 3 * MIB + 5

@@ -1,0 +1,294 @@
+"""GPU: sf_index_fds_blocks -- the reference's default mode over many files as
+ONE pipeline (index_path -> index_file per file, src/index.rs:685-715 ->
+610-659): every file cut by the caller's chunker on its own open descriptor,
+read again with pread into packed pinned stages, one sort + one explicit-list
+kernel launch per stage.
+
+* A tree of 0-B, 1-B, 32 KiB-capped, CDC-like and larger-than-a-stage files:
+  every row and every blocks_hash equal to the oracle's, at several stage
+  sizes, with and without stamps.
+* A file rewritten while the call reads it (a read hook between stages) is
+  named by bad_file with SF_EAGAIN; every other file's rows stay equal to the
+  oracle's.  A stale stamp, a list past the end, offsets going backwards and
+  a pipe fail for their file alone."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+from syncfast_amd import _lib, host
+
+pytestmark = pytest.mark.gpu
+
+KIB, MIB = 1 << 10, 1 << 20
+
+
+def _cdc_like_sizes(n, seed, mean=8192, cap=32768):
+    if n == 0:
+        return np.zeros(0, np.uint32)
+    rng = np.random.default_rng(seed)
+    sizes = np.minimum(rng.geometric(1.0 / mean, size=n // 64 + 16), cap)
+    cuts = np.cumsum(sizes)
+    cuts = cuts[cuts < n]
+    return np.diff(np.concatenate([[0], cuts, [n]])).astype(np.uint32)
+
+
+def _offs(sizes):
+    o = np.zeros(len(sizes), np.uint64)
+    if len(sizes):
+        o[1:] = np.cumsum(sizes.astype(np.uint64))[:-1]
+    return o
+
+
+def _tree(tmp_path, lens, seed):
+    files = []
+    for k, n in enumerate(lens):
+        p = tmp_path / f"f{k:04d}"
+        data = oracle.splitmix_bytes(n, seed + k).tobytes() if n else b""
+        p.write_bytes(data)
+        sizes = _cdc_like_sizes(n, seed + 1000 + k)
+        files.append((p, data, _offs(sizes), sizes))
+    return files
+
+
+def _check(files, rows, first, hashes, status, skip=()):
+    for k, (_p, data, offs, sizes) in enumerate(files):
+        if k in skip:
+            continue
+        assert status[k] == 0, k
+        mine = rows[int(first[k]):int(first[k + 1])]
+        assert mine.shape[0] == len(sizes)
+        dig = oracle.index_blocks(np.frombuffer(data, np.uint8), offs, sizes) if len(sizes) else \
+            np.zeros((0, 20), np.uint8)
+        assert np.array_equal(mine["sha1"], dig), k
+        assert np.array_equal(mine["offset"], offs) and np.array_equal(mine["size"], sizes), k
+        assert bytes(hashes[k]) == oracle.blocks_hash(dig), k
+
+
+def _run(files, stamps=True, stage_bytes=0):
+    fs = [open(p, "rb") for p, *_ in files]
+    try:
+        st = [host.file_stamp(f.fileno()) for f in fs] if stamps else None
+        return host.index_fds_blocks([f.fileno() for f in fs], [(o, s) for _p, _d, o, s in files], st,
+                                     stage_bytes=stage_bytes)
+    finally:
+        for f in fs:
+            f.close()
+
+
+@pytest.mark.parametrize("stage_bytes", [0, 1 * MIB, 300 * KIB])
+def test_tree_equals_oracle(gpu, tmp_path, stage_bytes):
+    """0-B, 1-B, one capped block, CDC-like files of 1 B .. 3 MiB and a file
+    larger than the stage (several windows, blocks_hash streamed over them)."""
+    lens = [0, 1, 32768, 32769, 0, 5, 100_000, 3 * MIB + 17, 64, 200 * KIB, 1, 0, 777_777, 16, 2 * MIB]
+    files = _tree(tmp_path, lens, 7000)
+    rows, first, hashes, status = _run(files, stage_bytes=stage_bytes)
+    assert int(first[-1]) == sum(len(s) for *_r, s in files)
+    _check(files, rows, first, hashes, status)
+    assert bytes(hashes[0]).hex() == "da39a3ee5e6b4b0d3255bfef95601890afd80709"  # no blocks: SHA1("")
+
+
+def test_many_small_files_and_reference_kat(gpu, tmp_path):
+    """600 files of 0-200 KiB in several stages, and the reference KAT file's
+    three blocks among them (src/index.rs:747-793)."""
+    rng = np.random.default_rng(7100)
+    lens = [int(x) for x in rng.integers(0, 200 * KIB, 600)]
+    files = _tree(tmp_path, lens, 7100)
+    k = tmp_path / "kat"
+    k.write_bytes(oracle.kat_input())
+    files.insert(300, (k, oracle.kat_input(), np.array([0, 11579, 44347], np.uint64),
+                       np.array([11579, 32768, 546], np.uint32)))
+    rows, first, hashes, status = _run(files, stage_bytes=8 * MIB)
+    _check(files, rows, first, hashes, status)
+    assert bytes(hashes[300]).hex() == "84c25d78edcdb67631639c43604cf0149564f044"
+
+
+def test_odd_lists(gpu, tmp_path):
+    """Lists a chunker would not make but the contract allows: gaps, overlaps,
+    empty blocks, blocks not covering the file, a 4 KiB fixed-like list."""
+    data = oracle.splitmix_bytes(300_000, 7200).tobytes()
+    p = tmp_path / "a"
+    p.write_bytes(data)
+    lists = [
+        (np.array([0, 0, 10, 10, 5000, 299_999], np.uint64), np.array([0, 100, 0, 50_000, 7, 1], np.uint32)),
+        (np.arange(0, 299_000, 4096, dtype=np.uint64), np.full(73, 4096, np.uint32)),
+        (np.array([123_456], np.uint64), np.array([176_544], np.uint32)),
+    ]
+    files = [(p, data, o, s) for o, s in lists]
+    rows, first, hashes, status = _run(files, stage_bytes=64 * KIB)
+    _check(files, rows, first, hashes, status)
+
+
+def test_rewritten_mid_call_is_named_and_others_exact(gpu, tmp_path):
+    """A file in a later stage is rewritten (same size, mtime restored: only
+    the ctime moves) right after stage 0 is read: SF_EAGAIN for that file,
+    bad_file = its index; every other file equals the oracle."""
+    lens = [400 * KIB] * 12
+    files = _tree(tmp_path, lens, 7300)
+    victim = 9
+    fired = []
+
+    def hook(stage):
+        if stage == 0 and not fired:
+            fired.append(stage)
+            time.sleep(0.02)  # past the filesystem clock's tick
+            p = files[victim][0]
+            st = os.stat(p)
+            with open(p, "r+b") as g:
+                g.seek(1000)
+                g.write(b"\x5A" * 3000)
+            os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns))
+
+    _lib.set_read_hook(hook)
+    try:
+        rows, first, hashes, status = _run(files, stage_bytes=1 * MIB)
+    finally:
+        _lib.set_read_hook(None)
+    assert fired
+    assert status[victim] == _lib.SF_EAGAIN and bytes(hashes[victim]) == bytes(20)
+    _check(files, rows, first, hashes, status, skip=(victim,))
+    # the raw call names it
+    fs = [open(p, "rb") for p, *_ in files]
+    try:
+        import ctypes
+        n = len(files)
+        bad = ctypes.c_uint32(99)
+        offs = [np.ascontiguousarray(o) for _p, _d, o, _s in files]
+        szs = [np.ascontiguousarray(s) for *_r, s in files]
+        po = (ctypes.c_void_p * n)(*[o.ctypes.data for o in offs])
+        pz = (ctypes.c_void_p * n)(*[z.ctypes.data for z in szs])
+        nb = np.array([o.size for o in offs], np.uint64)
+        stamps = (_lib.FileStamp * n)(*[host.file_stamp(f.fileno()) for f in fs])
+        with open(files[4][0], "r+b") as g:  # stale stamp for file 4
+            time.sleep(0.02)
+            g.write(b"\x01")
+        total = int(nb.sum())
+        out = np.zeros(total, host.SIG_DTYPE)
+        first2 = np.zeros(n + 1, np.uint64)
+        hh = np.zeros((n, 20), np.uint8)
+        fda = np.array([f.fileno() for f in fs], np.int32)
+        rc = _lib.lib().sf_index_fds_blocks(fda.ctypes.data, stamps, n, po, pz, nb.ctypes.data, 0,
+                                            out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig)), total,
+                                            first2.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), hh.ctypes.data,
+                                            None, ctypes.byref(bad))
+        assert rc == _lib.SF_EAGAIN and bad.value == 4
+    finally:
+        for f in fs:
+            f.close()
+
+
+def test_per_file_failures(gpu, tmp_path):
+    """A stale stamp, a list past the end, offsets going backwards and a pipe
+    fail for their own file; the others are exact."""
+    lens = [50_000, 60_000, 70_000, 80_000, 90_000]
+    files = _tree(tmp_path, lens, 7400)
+    fs = [open(p, "rb") for p, *_ in files]
+    r, w = os.pipe()
+    try:
+        stamps = [host.file_stamp(f.fileno()) for f in fs]
+        lists = [(o, s) for _p, _d, o, s in files]
+        with open(files[0][0], "r+b") as g:  # file 0 written after its stamp
+            time.sleep(0.02)
+            g.write(b"\x00" * 10)
+        o1, s1 = lists[1]
+        s1 = s1.copy()
+        s1[-1] += 1  # file 1: last block one byte past the end
+        lists[1] = (o1, s1)
+        o3, s3 = lists[3]
+        if len(o3) > 2:  # file 3: offsets going backwards
+            o3 = o3.copy()
+            o3[1], o3[2] = o3[2], o3[1]
+        lists[3] = (o3, s3)
+        fds = [f.fileno() for f in fs]
+        fds[4] = r  # file 4: a pipe
+        lists[4] = (np.array([0], np.uint64), np.array([1], np.uint32))
+        rows, first, hashes, status = host.index_fds_blocks(fds, lists, stamps[:4] + [host.file_stamp(r)])
+    finally:
+        for f in fs:
+            f.close()
+        os.close(r)
+        os.close(w)
+    assert list(status) == [_lib.SF_EAGAIN, _lib.SF_ERANGE, 0, _lib.SF_EINVAL, _lib.SF_EINVAL]
+    _check(files, rows, first, hashes, status, skip=(0, 1, 3, 4))
+
+
+def test_descriptor_position_unused(gpu, tmp_path):
+    files = _tree(tmp_path, [123_457, 1], 7500)
+    fs = [open(p, "rb") for p, *_ in files]
+    try:
+        fs[0].read(1000)
+        rows, first, hashes, status = host.index_fds_blocks([f.fileno() for f in fs],
+                                                            [(o, s) for _p, _d, o, s in files])
+        assert fs[0].tell() == 1000
+    finally:
+        for f in fs:
+            f.close()
+    _check(files, rows, first, hashes, status)
+
+
+def _toy_chunker(f):
+    """A content-defined stand-in over the open file (cut after a byte whose
+    low 12 bits of a running sum hit 0, 32 KiB cap), as a stream chunker."""
+    data = np.frombuffer(f.read(), np.uint8)
+    sizes, start = [], 0
+    h = np.cumsum(data.astype(np.uint64) * np.uint64(2654435761)) & np.uint64(0xFFF) if data.size else data
+    cuts = np.nonzero(h == 0)[0] if data.size else []
+    for c in cuts:
+        while c + 1 - start > 32768:
+            sizes.append(32768)
+            start += 32768
+        if c + 1 > start:
+            sizes.append(int(c + 1 - start))
+            start = int(c + 1)
+    while data.size - start > 32768:
+        sizes.append(32768)
+        start += 32768
+    if data.size > start:
+        sizes.append(int(data.size - start))
+    return sizes
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_index_path_default_mode_on_the_gpu(gpu, tmp_path, threads):
+    """Index.index_path with BoundaryChunker(stream=True): files cut on a pool,
+    batches through sf_index_fds_blocks; a file rewritten while its batch is
+    read is indexed again in its place.  Every stored row and blocks_hash
+    equals the oracle's over the file's bytes at the end."""
+    from syncfast_amd.index import BoundaryChunker, Index
+    root = tmp_path / "tree"
+    (root / "d").mkdir(parents=True)
+    rng = np.random.default_rng(7600)
+    names = [f"d/f{k:03d}" if k % 3 else f"g{k:03d}" for k in range(80)]
+    for k, n in enumerate(names):
+        (root / n).write_bytes(oracle.splitmix_bytes(int(rng.integers(0, 300 * KIB)), 7600 + k).tobytes())
+    victim = root / names[60]
+    fired = []
+
+    def hook(stage):
+        if stage == 0 and not fired:
+            fired.append(stage)
+            time.sleep(0.02)
+            victim.write_bytes(oracle.splitmix_bytes(123_457, 7699).tobytes())
+
+    idx = Index.open(root / ".syncfast.idx", chunker=BoundaryChunker(_toy_chunker, stream=True))
+    _lib.set_read_hook(hook)
+    try:
+        idx.index_path(root, batch_bytes=2 * MIB, chunk_threads=threads)
+    finally:
+        _lib.set_read_hook(None)
+    idx.commit()
+    assert fired
+    for n in names:
+        data = (root / n).read_bytes()
+        fid, _m, bh = idx.get_file(n)
+        rows = idx.list_file_blocks(fid)
+        sizes = np.asarray([s for _h, _o, s in rows], np.uint32)
+        offs = np.asarray([o for _h, o, _s in rows], np.uint64)
+        with open(root / n, "rb") as f:
+            assert sizes.tolist() == _toy_chunker(f), n
+        dig = oracle.index_blocks(np.frombuffer(data, np.uint8), offs, sizes) if len(sizes) else \
+            np.zeros((0, 20), np.uint8)
+        assert [h.bytes for h, _o, _s in rows] == [bytes(d) for d in dig], n
+        assert bh.bytes == oracle.blocks_hash(dig) and idx.compute_blocks_hash(fid) == bh, n

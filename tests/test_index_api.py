@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 import oracle
+from syncfast_amd import _lib
 from syncfast_amd.digest import HashDigest, InvalidHashDigest
 from syncfast_amd.index import BoundaryChunker, FixedChunker, Index, temp_name, untemp_name
 
@@ -375,6 +376,19 @@ def _oracle_device_calls(monkeypatch):
     monkeypatch.setattr(host, "index_fd_blocks",
                         lambda fd, offs, sizes, stamp=None: rows_of(_pread_all(fd), offs, sizes))
 
+    def fds_rows(fds, lists, stamps=None, stage_bytes=0):
+        parts, first, hashes = [], [0], []
+        for fd, (offs, sizes) in zip(fds, lists):
+            rows, bh = rows_of(_pread_all(fd), offs, sizes)
+            parts.append(rows)
+            first.append(first[-1] + rows.shape[0])
+            hashes.append(np.frombuffer(bh, np.uint8))
+        rows = np.concatenate(parts) if parts else np.zeros(0, host.SIG_DTYPE)
+        return (rows, np.asarray(first, np.uint64), np.asarray(hashes, np.uint8).reshape(-1, 20),
+                np.zeros(len(fds), np.int32))
+
+    monkeypatch.setattr(host, "index_fds_blocks", fds_rows)
+
 
 def _pread_all(fd):
     """The whole file open on fd, read with pread (the descriptor's position
@@ -493,3 +507,104 @@ def test_boundary_rows_read_back_on_the_gpu(gpu, tmp_path, stream):
     idx.index_path(root)
     idx.commit()
     _check_read_back(idx, root, files, _toy_cdc)
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+@pytest.mark.parametrize("batch_bytes", [0, 1 << 30, 20_000])
+def test_index_path_stream_chunker_many_files(tmp_path, monkeypatch, threads, batch_bytes):
+    """index_path in the reference's default mode (BoundaryChunker(stream=True)):
+    files cut on a thread pool, batches through sf_index_fds_blocks (the oracle
+    stands in for the device here); rows, blocks_hash and file_ids (walk order)
+    equal the file-by-file path's."""
+    _oracle_device_calls(monkeypatch)
+    root = tmp_path / "tree"
+    files = _tree(root, 4300)
+    for k in range(20):
+        (root / f"x{k:02d}").write_bytes(oracle.splitmix_bytes(3000 * k, 4400 + k).tobytes())
+    idx = Index.open(root / ".syncfast.idx", chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
+    idx.index_path(root, batch_bytes=batch_bytes, chunk_threads=threads)
+    idx.commit()
+    ref = Index.open_in_memory(chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
+    ref.index_path(root, batch_bytes=0)
+    ref.commit()
+    assert idx.db.execute("SELECT file_id, name FROM files ORDER BY file_id").fetchall() == \
+        ref.db.execute("SELECT file_id, name FROM files ORDER BY file_id").fetchall()
+    q = "SELECT file_id, hash, offset, size, present FROM blocks ORDER BY rowid"
+    assert idx.db.execute(q).fetchall() == ref.db.execute(q).fetchall()
+    q = "SELECT file_id, blocks_hash FROM files ORDER BY file_id"
+    assert idx.db.execute(q).fetchall() == ref.db.execute(q).fetchall()
+    _check_read_back(idx, root, files, _toy_cdc)
+    _check_read_back(idx, root, [f"x{k:02d}" for k in range(20)], None)
+    before = idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0]
+    idx.index_path(root, batch_bytes=batch_bytes, chunk_threads=threads)  # mtimes unchanged: nothing again
+    assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
+
+
+def test_index_path_stream_chunker_file_changed_is_reindexed(tmp_path, monkeypatch):
+    """A file the many-file call reports SF_EAGAIN for (written while it was
+    read) is indexed again in its place; its rows are the new bytes'."""
+    from syncfast_amd import host
+    _oracle_device_calls(monkeypatch)
+    root = tmp_path / "tree"
+    files = _tree(root, 4500)
+    real = host.index_fds_blocks
+    victim = root / "sub" / "b.bin"
+
+    def fake(fds, lists, stamps=None, stage_bytes=0):
+        rows, first, hashes, status = real(fds, lists, stamps, stage_bytes)
+        for k, fd in enumerate(fds):
+            if os.fstat(fd).st_ino == os.stat(victim).st_ino and not fake.done:
+                fake.done = True
+                status[k] = _lib.SF_EAGAIN
+                hashes[k] = 0
+                victim.write_bytes(oracle.splitmix_bytes(22_222, 4599).tobytes())
+        return rows, first, hashes, status
+    fake.done = False
+    monkeypatch.setattr(host, "index_fds_blocks", fake)
+    idx = Index.open_in_memory(chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
+    idx.index_path(root)
+    assert fake.done
+    _check_read_back(idx, root, files, _toy_cdc)
+    fid = idx.get_file("sub/b.bin")[0]
+    assert sum(s for _h, _o, s in idx.list_file_blocks(fid)) == 22_222
+
+
+@pytest.mark.parametrize("mode", ["boundary", "fixed"])
+def test_index_file_that_keeps_changing_falls_back_to_one_pass(tmp_path, monkeypatch, mode):
+    """a file that changes on every attempt (a log being appended
+    to) is not an error: after CHANGED_RETRIES attempts index_file hashes the
+    bytes of ONE read, as the reference's single pass does
+    (src/index.rs:615-647), and index_path goes on."""
+    from syncfast_amd import host
+    from syncfast_amd.index import CHANGED_RETRIES
+    _oracle_device_calls(monkeypatch)
+    p = tmp_path / "log"
+    p.write_bytes(oracle.splitmix_bytes(30_000, 4600).tobytes())
+    calls = {"n": 0}
+
+    def always_changed(*_a, **_k):
+        calls["n"] += 1
+        with open(p, "ab") as g:
+            g.write(b"line\n")
+        raise _lib.SfError(_lib.SF_EAGAIN, "changed")
+
+    monkeypatch.setattr(host, "index_fd_blocks", always_changed)
+    monkeypatch.setattr(host, "index_fd_fixed", always_changed)
+
+    def buffer_rows(data, bs):
+        offs, sizes, dig = oracle.index_fixed(np.frombuffer(bytes(data), np.uint8), bs)
+        rows = np.zeros(len(offs), host.SIG_DTYPE)
+        rows["offset"], rows["size"], rows["sha1"] = offs, sizes, dig
+        return rows
+
+    monkeypatch.setattr(host, "index_buffer", buffer_rows)
+    ch = BoundaryChunker(_stream_toy_cdc, stream=True) if mode == "boundary" else FixedChunker(4096)
+    idx = Index.open_in_memory(chunker=ch)
+    idx.index_file(p, "log")
+    assert calls["n"] == CHANGED_RETRIES
+    data = p.read_bytes()
+    fid, _m, bh = idx.get_file("log")
+    rows = idx.list_file_blocks(fid)
+    assert b"".join(data[o:o + s] for _h, o, s in rows) == data
+    assert all(hashlib.sha1(data[o:o + s]).digest() == h.bytes for h, o, s in rows)
+    assert idx.compute_blocks_hash(fid) == bh
