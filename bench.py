@@ -108,6 +108,9 @@ def parse():
     p.add_argument("--no-cdc-list", action="store_true",
                    help="skip the content-defined-like list leg (config 2 at N=1: the reference's default block "
                         "shape through the explicit-list kernel, not `value`)")
+    p.add_argument("--no-default-mode", action="store_true",
+                   help="skip the default-mode leg (config 2 at N=1: the reference's content-defined mode over "
+                        "many files on disk through sf_index_fds_blocks, with the stand-in chunker; not `value`)")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--gather-root", default="rotate", choices=("rotate", "fixed"),
                    help="rank that receives each step's tables: rotates over the ranks, the last step's being "
@@ -324,6 +327,134 @@ def config1_default_mode_e2e():
                      "sf_index_fd_blocks on the same fd (pread windows, H2D, sha1_table_kernel, D2H rows + "
                      "blocks_hash)",
             "label": "stand-in chunker: the crate's per-byte work, not its boundaries"}
+
+
+DEFAULT_MODE_TREES = {
+    # config 3's shape: 1024 files of 8 MiB (BASELINE configs[2]); a tree of 0-200 KiB files
+    "c3_1024x8MiB": [8 << 20] * 1024,
+    "small_0_200KiB": "small",
+}
+SMALL_TREE_BYTES = 1 << 30
+PER_FILE_SAMPLE_BYTES = 512 << 20  # the per-file loop is timed on the tree's first ~512 MiB
+
+
+def _sf_index_run(exe, args, paths, timeout=600):
+    r = subprocess.run([exe] + args + paths, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"sf_index {' '.join(args)} failed ({r.returncode}): {r.stderr.strip()[-300:]}")
+    return r
+
+
+def _parse_files(out):
+    """sf_index's stdout -> {path: (rows or None, blocks_hash hex)}."""
+    res, cur, rows = {}, None, None
+    for ln in out.splitlines():
+        if ln.startswith("file "):
+            cur, rows = ln.split()[1], []
+        elif ln.startswith("blocks_hash "):
+            res[cur] = (rows if rows else None, ln.split()[1])
+        elif rows is not None and ln and ln[0].isdigit():
+            o, s, h = ln.split()
+            rows.append((int(o), int(s), h))
+    return res
+
+
+def default_mode_files(data, budget_threads):
+    """Not `value`: the reference's DEFAULT mode over many files on disk
+    (index_path -> index_file per file, src/index.rs:685-715 -> 610-659),
+    end to end: files in the page cache -> the stand-in chunker (the crate's
+    per-byte work, not its boundaries) on 1 and on N host threads, each file
+    opened once and cut over its descriptor -> every batch of ~256 MiB of cut
+    files through ONE sf_index_fds_blocks call (pread windows into packed
+    pinned stages, one sort + one sha1_table_kernel launch per stage, rows +
+    blocks_hash) while the threads cut the next batch (examples/build/sf_index
+    -Z -M).  Beside it today's per-file loop (sf_index -Z: chunk, then one
+    sf_index_fd_blocks call per file), timed on the tree's first ~512 MiB.
+    Self-checks: every file's blocks_hash equal across the routes; the first
+    and last file's rows re-hashed with the product's host SHA-1."""
+    import numpy as np
+    import random
+    import tempfile
+    from syncfast_amd import host
+    exe = os.path.join(ROOT, "examples", "build", "sf_index")
+    if not os.access(exe, os.X_OK):
+        return {"status": "examples/build/sf_index not built"}
+    out = {"label": "stand-in chunker: the crate's per-byte work, not its boundaries",
+           "route": "files (page cache) -> chunker threads over the open fds -> sf_index_fds_blocks per ~256 MiB "
+                    "batch (overlapped with cutting the next) -> rows + blocks_hash",
+           "threads_max": budget_threads}
+    host_bytes = data.cpu() if data.numel() <= (8 << 30) else data[: 8 << 30].cpu()
+    hb = host_bytes.numpy()
+    rng = np.random.default_rng(11)
+    for name, spec in DEFAULT_MODE_TREES.items():
+        d = tempfile.mkdtemp(prefix="sf_dm_")
+        try:
+            if spec == "small":
+                lens, tot = [], 0
+                while tot < SMALL_TREE_BYTES:
+                    n = int(rng.integers(0, 200 << 10))
+                    lens.append(n)
+                    tot += n
+            else:
+                lens = spec
+            paths, pos = [], 0
+            for k, n in enumerate(lens):
+                p = os.path.join(d, f"f{k:05d}")
+                a0 = pos % (hb.size - n) if hb.size > n else 0
+                hb[a0: a0 + n].tofile(p)
+                pos += n + 4099
+                paths.append(p)
+            total = sum(lens)
+            leg = {"files": len(lens), "bytes": total}
+            print(f"bench.py: default mode {name}: {len(lens)} files written", file=sys.stderr, flush=True)
+            hashes = {}
+            for j in (budget_threads, budget_threads, 1):
+                r = _sf_index_run(exe, ["-Z", "-M", "-q", "-T", "-j", str(j)], paths)
+                t = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")][-1]
+                print(f"bench.py: default mode {name}, {j} chunker threads: {t['wall_s']:.3f} s", file=sys.stderr,
+                      flush=True)
+                res = _parse_files(r.stdout)
+                if not hashes:
+                    hashes = {p: h for p, (_rows, h) in res.items()}
+                    for p in (paths[0], paths[-1]):  # full rows: re-hash them
+                        rows = res[p][0] or []
+                        raw = np.fromfile(p, np.uint8)
+                        assert sum(s for _o, s, _h in rows) == raw.size, "rows do not tile the file"
+                        for o, s, h in random.Random(5).sample(rows, min(32, len(rows))):
+                            assert host.sha1(raw[o:o + s]).hex() == h, "row self-check failed"
+                        dig = np.frombuffer(b"".join(bytes.fromhex(h) for _o, _s, h in rows), np.uint8)
+                        assert host.blocks_hash(dig).hex() == res[p][1], "blocks_hash self-check failed"
+                assert {p: h for p, (_rows, h) in res.items()} == hashes, "routes disagree on a blocks_hash"
+                key = f"threads_{j}"
+                prev = leg.get(key)
+                gbs = total / t["wall_s"] / 1e9
+                if prev is None or gbs > prev["e2e_GB/s"]:
+                    leg[key] = {"e2e_GB/s": round(gbs, 3), "wall_s": round(t["wall_s"], 4),
+                                "hash_call_s": round(t["hash_call_s"], 4), "chunk_cpu_s": round(t["chunk_cpu_s"], 4),
+                                "wait_for_cut_s": round(t["wait_cut_s"], 4), "batches": t["batches"],
+                                "blocks": t["blocks"]}
+            # today's per-file loop on a sample
+            sample, sb = [], 0
+            for p, n in zip(paths, lens):
+                if sb >= PER_FILE_SAMPLE_BYTES:
+                    break
+                sample.append(p)
+                sb += n
+            r = _sf_index_run(exe, ["-Z", "-T"], sample)
+            ts = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")]
+            res = _parse_files(r.stdout)
+            assert all(res[p][1] == hashes[p] for p in sample), "per-file loop disagrees on a blocks_hash"
+            c = sum(x["chunk_s"] for x in ts)
+            h = sum(x["hash_s"] for x in ts)
+            leg["per_file_loop"] = {"e2e_GB/s": round(sb / (c + h) / 1e9, 3), "files": len(sample), "bytes": sb,
+                                    "chunk_s": round(c, 4), "hash_calls_s": round(h, 4),
+                                    "note": "one thread: chunk a file, then one sf_index_fd_blocks call for it"}
+            j16 = leg[f"threads_{budget_threads}"]
+            leg["chunker_share"] = round(min(1.0, j16["chunk_cpu_s"] / budget_threads / j16["wall_s"]), 4)
+            out[name] = leg
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 def cpu_baseline(nbytes_total, bs, budget_s):
@@ -762,6 +893,9 @@ def main():
     e2e = None
     if not a.no_e2e and world == 1 and files is None and weaks is None:
         e2e = e2e_host_buffer(torch, data, d, bs)
+    dmode = None
+    if not a.no_default_mode and world == 1 and files is None and weaks is None and a.config == 2:
+        dmode = default_mode_files(data, max(1, min(16, len(os.sched_getaffinity(0)))))
     cpu = cpu_all = cpu_ni = cpu_ni_all = None
     config1 = config1_probe() if world == 1 else None
     if not a.no_cpu_baseline and world == 1:
@@ -816,6 +950,7 @@ def main():
         "blocks_hash_host_ms": round(bh_ms, 2) if bh_ms is not None else None,
         "e2e_host_buffer": e2e,
         "content_defined_list": cdc,
+        "default_mode_files": dmode,
     }
     print(json.dumps(line), flush=True)
     if distributed:

@@ -23,15 +23,21 @@
  *     -Z: the drop-in's default splice: each file opened once, streamed
  *     through a boundary chunker (the stand-in of zpaq_standin.h in place of
  *     the cdchunking crate), its list hashed from the same descriptor
- *     (sf_index_fd_blocks); -T adds a timing line per file on stderr.
+ *     (sf_index_fd_blocks); -T adds a timing line per file on stderr;
+ *     -Z -M: the default mode over many files (index_path): the files cut by
+ *     -j N chunker threads, every batch of ~-S MiB of cut files hashed by ONE
+ *     sf_index_fds_blocks call while the threads cut the next batch; -q
+ *     prints only the first and last file's rows (every file's blocks_hash).
  * Regular files (default mode) go through the same one-open form:
  * sf_file_stamp_fd + sf_index_fd_fixed on the open descriptor.
  */
 #include <errno.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
@@ -294,6 +300,238 @@ static int index_zpaq(const char *path, int timing) {
     return rc;
 }
 
+/* The stand-in chunker over an open file from its start (64 KiB reads, as
+ * index_zpaq): the (offset, size) list, grown with realloc; *total = bytes
+ * read.  SF_OK or SF_EIO / SF_ENOMEM. */
+static int zpaq_cut_fd(int fd, uint8_t *buf, size_t bufsz, uint64_t **offs_io, uint32_t **sizes_io, uint64_t *cap_io,
+                       uint64_t *n_out, uint64_t *total_out, double *read_s) {
+    uint64_t *offs = *offs_io, cap = *cap_io, n = 0, total = 0, start = 0;
+    uint32_t *sizes = *sizes_io;
+    int rc = SF_OK;
+    sf_zpaq z;
+    sf_zpaq_init(&z, 13, 32768); /* ZPAQ_BITS, MAX_BLOCK_SIZE: src/index.rs:40-41 */
+    for (int eof = 0; rc == SF_OK && !eof;) {
+        const double t0 = now_s();
+        const ssize_t r = pread(fd, buf, bufsz, (off_t)total);
+        *read_s += now_s() - t0;
+        if (r < 0 && errno == EINTR) continue;
+        if (r < 0) { rc = SF_EIO; break; }
+        uint64_t p = 0;
+        for (;;) {
+            const size_t k = r > 0 ? sf_zpaq_next(&z, buf + p, (size_t)((uint64_t)r - p)) : 0;
+            eof = r == 0;
+            if (k == 0 && !(eof && total > start)) break;
+            const uint64_t end = k ? total + p + k : total;
+            if (n == cap) {
+                const uint64_t c2 = cap ? 2 * cap : 1024;
+                uint64_t *o2 = realloc(offs, c2 * sizeof(uint64_t));
+                if (o2) offs = o2;
+                uint32_t *s2 = o2 ? realloc(sizes, c2 * sizeof(uint32_t)) : NULL;
+                if (s2) sizes = s2;
+                if (!o2 || !s2) { rc = SF_ENOMEM; break; }
+                cap = c2;
+            }
+            offs[n] = start;
+            sizes[n++] = (uint32_t)(end - start);
+            start = end;
+            if (!k) break;
+            p += k;
+        }
+        total += r > 0 ? (uint64_t)r : 0;
+    }
+    *offs_io = offs;
+    *sizes_io = sizes;
+    *cap_io = cap;
+    *n_out = n;
+    *total_out = total;
+    return rc;
+}
+
+/* -Z -M: index_path's default mode from C.  Files are stat'ed and dealt into
+ * batches of about batch_bytes; `threads` chunker threads take the files in
+ * order (opening each once, stamping it, cutting it over the open descriptor)
+ * but never more than one batch ahead of the hashing; the main thread hashes
+ * each batch with ONE sf_index_fds_blocks on those descriptors as soon as all
+ * its files are cut.  A file the call reports SF_EAGAIN for (written
+ * meanwhile) is cut and hashed again alone through index_zpaq's retry loop.
+ * -T: one JSON line on stderr with the wall time and its parts. */
+typedef struct {
+    const char *path;
+    int fd, rc;
+    sf_file_stamp st;
+    uint64_t *offs, cap, n, bytes;
+    uint32_t *sizes;
+} cut_job;
+
+typedef struct {
+    cut_job *jobs;
+    int n, threads;
+    const int *batch_of;     /* file -> batch */
+    int *batch_left;         /* files of each batch still being cut */
+    int next, hashed;        /* next file to cut; the last batch hashed */
+    double chunk_s, open_s, read_s; /* summed over threads: cutting (all of it), its open + stamp, its reads */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} cut_pool;
+
+static void *cut_worker(void *arg) {
+    cut_pool *P = arg;
+    enum { kRead = 1 << 16 };
+    uint8_t *buf = malloc(kRead);
+    for (;;) {
+        pthread_mutex_lock(&P->mu);
+        /* at most one batch ahead of the one being hashed (hashed + 1) */
+        while (P->next < P->n && P->batch_of[P->next] > P->hashed + 2) pthread_cond_wait(&P->cv, &P->mu);
+        const int k = P->next < P->n ? P->next++ : -1;
+        pthread_mutex_unlock(&P->mu);
+        if (k < 0) break;
+        cut_job *j = &P->jobs[k];
+        const double t0 = now_s();
+        j->fd = open(j->path, O_RDONLY);
+        j->rc = j->fd < 0 ? SF_EIO : !buf ? SF_ENOMEM : sf_file_stamp_fd(j->fd, &j->st);
+        const double t1 = now_s();
+        double rd = 0;
+        if (j->rc == SF_OK) j->rc = zpaq_cut_fd(j->fd, buf, kRead, &j->offs, &j->sizes, &j->cap, &j->n, &j->bytes, &rd);
+        if (j->rc == SF_OK && j->bytes != j->st.size) j->rc = SF_EAGAIN;  /* written while cut */
+        const double dt = now_s() - t0;
+        pthread_mutex_lock(&P->mu);
+        P->chunk_s += dt;
+        P->open_s += t1 - t0;
+        P->read_s += rd;
+        P->batch_left[P->batch_of[k]]--;
+        pthread_cond_broadcast(&P->cv);
+        pthread_mutex_unlock(&P->mu);
+    }
+    free(buf);
+    return NULL;
+}
+
+static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, int timing, int quiet) {
+    cut_job *jobs = calloc((size_t)(n ? n : 1), sizeof(cut_job));
+    int *batch_of = malloc((size_t)(n ? n : 1) * sizeof(int)), nb = 0;
+    int *batch_left = calloc((size_t)(n ? n : 1), sizeof(int)), *batch_first = calloc((size_t)n + 2, sizeof(int));
+    if (!jobs || !batch_of || !batch_left || !batch_first) return SF_ENOMEM;
+    const double t_start = now_s();
+    uint64_t acc = 0, total_bytes = 0, total_blocks = 0;
+    /* three batches' descriptors may be open at once (one hashed, one cut,
+     * one waiting): a batch holds at most a quarter of the descriptor limit */
+    struct rlimit rl;
+    int max_files = 4096;
+    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY && (int)(rl.rlim_cur / 4) < max_files)
+        max_files = rl.rlim_cur / 4 > 16 ? (int)(rl.rlim_cur / 4) : 16;
+    for (int k = 0; k < n; k++) { /* batches by size and descriptor count */
+        struct stat sb;
+        jobs[k].path = paths[k];
+        jobs[k].fd = -1;
+        const uint64_t sz = stat(paths[k], &sb) == 0 ? (uint64_t)sb.st_size : 0;
+        if (k == 0 || acc >= batch_bytes || k - batch_first[nb - 1] >= max_files) {
+            batch_first[nb++] = k;
+            acc = 0;
+        }
+        batch_of[k] = nb - 1;
+        batch_left[nb - 1]++;
+        acc += sz;
+    }
+    batch_first[nb] = n;
+    cut_pool P = {jobs, n, threads, batch_of, batch_left, 0, -1, 0.0, 0.0, 0.0, PTHREAD_MUTEX_INITIALIZER,
+                  PTHREAD_COND_INITIALIZER};
+    pthread_t *th = malloc((size_t)(threads > 0 ? threads : 1) * sizeof(pthread_t));
+    int started = 0, rc = th ? SF_OK : SF_ENOMEM;
+    for (int t = 0; rc == SF_OK && t < threads; t++)
+        if (pthread_create(&th[t], NULL, cut_worker, &P) == 0) started++;
+    if (started == 0) rc = SF_ENOMEM;
+    double t_wait = 0, t_hash = 0;
+    for (int b = 0; rc == SF_OK && b < nb; b++) {
+        const int f0 = batch_first[b], m = batch_first[b + 1] - f0;
+        const double tw = now_s();
+        pthread_mutex_lock(&P.mu);
+        while (batch_left[b] > 0) pthread_cond_wait(&P.cv, &P.mu);
+        pthread_mutex_unlock(&P.mu);
+        t_wait += now_s() - tw;
+        int *fds = malloc((size_t)m * sizeof(int)), *fst = malloc((size_t)m * sizeof(int));
+        sf_file_stamp *sts = malloc((size_t)m * sizeof(sf_file_stamp));
+        const uint64_t **po = malloc((size_t)m * sizeof(void *));
+        const uint32_t **pz = malloc((size_t)m * sizeof(void *));
+        uint64_t *cnt = malloc((size_t)m * sizeof(uint64_t)), *first = malloc(((size_t)m + 1) * sizeof(uint64_t));
+        uint8_t *hashes = malloc((size_t)m * 20);
+        uint64_t rows_n = 0;
+        for (int k = 0; k < m; k++) rows_n += jobs[f0 + k].rc == SF_OK ? jobs[f0 + k].n : 0;
+        sf_block_sig *rows = malloc((rows_n ? rows_n : 1) * sizeof(sf_block_sig));
+        if (!fds || !fst || !sts || !po || !pz || !cnt || !first || !hashes || !rows) rc = SF_ENOMEM;
+        for (int k = 0; rc == SF_OK && k < m; k++) {
+            const cut_job *j = &jobs[f0 + k];
+            if (j->rc != SF_OK && j->rc != SF_EAGAIN) { rc = j->rc; break; }
+            fds[k] = j->rc == SF_OK ? j->fd : -1; /* a file written while cut: indexed again below */
+            sts[k] = j->st;
+            po[k] = j->offs;
+            pz[k] = j->sizes;
+            cnt[k] = j->rc == SF_OK ? j->n : 0;
+        }
+        uint32_t bad = 0;
+        if (rc == SF_OK) {
+            const double th0 = now_s();
+            const int r = sf_index_fds_blocks(fds, sts, (uint32_t)m, po, pz, cnt, 0, rows, rows_n, first, hashes, fst,
+                                              &bad);
+            t_hash += now_s() - th0;
+            if (r != SF_OK && !(r == fst[bad])) rc = r; /* a per-file failure is handled per file */
+        }
+        for (int k = 0; rc == SF_OK && k < m; k++) {
+            cut_job *j = &jobs[f0 + k];
+            if (j->rc == SF_EAGAIN || fst[k] == SF_EAGAIN) { /* written meanwhile: once more, alone */
+                close(j->fd);
+                j->fd = -1;
+                if ((rc = index_zpaq(j->path, 0)) != SF_OK) break;
+                continue;
+            }
+            if (fst[k] != SF_OK) { rc = fst[k]; break; }
+            total_bytes += j->bytes;
+            total_blocks += cnt[k];
+            const int show = !quiet || f0 + k == 0 || f0 + k == n - 1;
+            if (show) print_rows(j->path, rows + first[k], cnt[k], hashes + 20 * k);
+            else {
+                char h[41];
+                hex(hashes + 20 * k, h);
+                printf("file %s blocks %llu\nblocks_hash %s\n", j->path, (unsigned long long)cnt[k], h);
+            }
+        }
+        for (int k = 0; k < m; k++) {
+            cut_job *j = &jobs[f0 + k];
+            if (j->fd >= 0) close(j->fd);
+            j->fd = -1;
+            free(j->offs);
+            free(j->sizes);
+            j->offs = NULL;
+            j->sizes = NULL;
+        }
+        free(fds); free(fst); free(sts); free(po); free(pz); free(cnt); free(first); free(hashes); free(rows);
+        pthread_mutex_lock(&P.mu);
+        P.hashed = b;
+        pthread_cond_broadcast(&P.cv);
+        pthread_mutex_unlock(&P.mu);
+    }
+    pthread_mutex_lock(&P.mu);
+    P.hashed = nb; /* on an error: release the workers */
+    P.next = rc == SF_OK ? P.next : n;
+    pthread_cond_broadcast(&P.cv);
+    pthread_mutex_unlock(&P.mu);
+    for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
+    for (int k = 0; k < n; k++) {
+        if (jobs[k].fd >= 0) close(jobs[k].fd);
+        free(jobs[k].offs);
+        free(jobs[k].sizes);
+    }
+    const double wall = now_s() - t_start;
+    if (timing && rc == SF_OK)
+        fprintf(stderr,
+                "{\"zpaq_many\": %d, \"threads\": %d, \"batches\": %d, \"bytes\": %llu, \"blocks\": %llu, "
+                "\"wall_s\": %.6f, \"chunk_cpu_s\": %.6f, \"open_s\": %.6f, \"read_s\": %.6f, \"hash_call_s\": %.6f, "
+                "\"wait_cut_s\": %.6f}\n",
+                n, threads, nb, (unsigned long long)total_bytes, (unsigned long long)total_blocks, wall, P.chunk_s,
+                P.open_s, P.read_s, t_hash, t_wait);
+    free(th); free(jobs); free(batch_of); free(batch_left); free(batch_first);
+    return rc;
+}
+
 /* -v N: the default mode's wire run from C: N synthetic bytes generated in
  * HBM, cut on the host by the stand-in chunker, hashed on the device as an
  * explicit list (sf_index_device_blocks), and the list's FILE_BLOCK run --
@@ -428,7 +666,8 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0;
+    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
+    uint64_t batch_mib = 256;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -436,6 +675,10 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-s") == 0) shards = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-w") == 0) wire = atoll(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-v") == 0) wire_cdc = atoll(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-j") == 0) threads = atoi(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
+        else if (strcmp(argv[i], "-M") == 0) many = 2;
+        else if (strcmp(argv[i], "-q") == 0) quiet = 1;
         else if (strcmp(argv[i], "-m") == 0) many = 1;
         else if (strcmp(argv[i], "-L") == 0) lookup = 1;
         else if (strcmp(argv[i], "-B") == 0) buffer = 1;
@@ -445,7 +688,8 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] | -s shards] path... | -w bytes | -v bytes | -L dst src\n",
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-q]] | -s shards] "
+                        "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
     }
@@ -471,6 +715,12 @@ int main(int argc, char **argv) {
     if (lookup) {
         const int rc = i + 2 == argc ? lookup_blocks(argv[i], argv[i + 1], bs) : SF_EINVAL;
         if (rc != SF_OK) fprintf(stderr, "lookup: %s\n", sf_strerror(rc));
+        sf_release_host_cache();
+        return rc != SF_OK;
+    }
+    if (many == 2 && zpaq) {
+        const int rc = index_zpaq_many(argv + i, argc - i, threads > 0 ? threads : 1, batch_mib << 20, timing, quiet);
+        if (rc != SF_OK) fprintf(stderr, "zpaq many: %s\n", sf_strerror(rc));
         sf_release_host_cache();
         return rc != SF_OK;
     }

@@ -395,6 +395,48 @@ int sf_index_fds_blocks(const int *fds, const sf_file_stamp *stamps, uint32_t n_
                         uint64_t stage_bytes, sf_block_sig *out, uint64_t cap, uint64_t *first_row,
                         uint8_t *blocks_hashes, int *file_status, uint32_t *bad_file);
 
+/* ------------------------------------------- one process, N devices ---- */
+
+/* Contiguous, block-aligned shard `shard` of n_shards of a file_len-byte file:
+ * bytes [*start, *start + *len).  Blocks are dealt as evenly as possible (the
+ * first nblocks % n_shards shards get one more); a shard may be empty.  The
+ * shards' rows concatenated in shard order are the file's rows.  The
+ * partition every multi-device form below uses (and syncfast_amd.shard's
+ * shard_range, one process per GPU). */
+int sf_shard_range(uint64_t file_len, uint32_t block_size, uint32_t n_shards, uint32_t shard, uint64_t *start,
+                   uint64_t *len);
+
+/* index_file (src/index.rs:610-659) of one regular file on N devices of this
+ * process: fixed tiling, shard r (sf_shard_range) read with pread from ONE
+ * open of the file and hashed on device r by a host thread of its own (each
+ * device on its own PCIe link, through the staged pipeline of sf_index_file),
+ * rows written straight into out at the shard's first row; then blocks_hash
+ * over every digest in order on the host (it chains over the whole file).
+ * n_devices = 0: every visible device; devices 0 .. n_devices-1 are used.
+ * The file is stamped at the open and again after the last read: SF_EAGAIN
+ * if it changed (the rows are not valid).  SF_ENOSPC with *n_out = the need
+ * when cap is too small (nothing read); SF_EINVAL if path is not a regular
+ * file or n_devices exceeds the visible devices.  The calling thread's current
+ * device is left as it was.  Blocking. */
+int sf_index_file_multi(const char *path, uint32_t block_size, uint32_t n_devices, sf_block_sig *out, uint64_t cap,
+                        uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
+/* The device-resident form on N devices of this process, the gather over
+ * xGMI inside the library: d_shards[r] (on device r) holds shard r
+ * (sf_shard_range of file_len, block_size, n_devices) of one logical file;
+ * each shard is hashed on its own device, on streams[r] (streams may be NULL:
+ * each device's null stream), the root's straight into its rows of d_table
+ * (device `root`, ceil(file_len / block_size) x 20 B), every other device's
+ * into d_digests[r] (its own scratch, its shard's rows x 20 B) and from there
+ * to its rows of d_table with RCCL (one communicator per device list,
+ * ncclCommInitAll on first use, kept; grouped ncclSend / ncclRecv, since the
+ * shards' row counts may differ by one).  Asynchronous: d_table is complete
+ * once streams[root] has run past the call.  Devices 0 .. n_devices-1; the
+ * caller's current device is left as it was.  SF_ENODEV if RCCL cannot be
+ * loaded or a communicator not made. */
+int sf_index_device_multi(uint32_t n_devices, const void *const *d_shards, uint64_t file_len, uint32_t block_size,
+                          void *const *d_digests, uint32_t root, void *d_table, void *const *streams);
+
 /* compute_blocks_hash (src/index.rs:661-682) on the host: SHA-1 over the
  * n 20-byte digests in order.  Sequential by definition; runs on a host
  * core (SHA-NI when the CPU has it). */

@@ -1,0 +1,67 @@
+"""Sweep of the default-mode many-file route (examples/build/sf_index -Z -M):
+chunker threads x the library's reader threads (SF_IO_THREADS) x batch size,
+on config 3's shape (1024 x 8 MiB) and a 0-200 KiB tree, files in the page
+cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
+
+usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...]"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+EXE = os.path.join(ROOT, "examples", "build", "sf_index")
+
+
+def write_tree(d, lens, seed):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
+    paths = []
+    for k, n in enumerate(lens):
+        p = os.path.join(d, f"f{k:05d}")
+        a = int(rng.integers(0, src.size - n)) if n < src.size else 0
+        src[a:a + n].tofile(p)
+        paths.append(p)
+    return paths
+
+
+def main():
+    js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "8,12,16").split(",")]
+    ios = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8,16").split(",")]
+    ss = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "256").split(",")]
+    rng = np.random.default_rng(3)
+    small, tot = [], 0
+    while tot < (1 << 30):
+        small.append(int(rng.integers(0, 200 << 10)))
+        tot += small[-1]
+    for name, lens in (("c3_1024x8MiB", [8 << 20] * 1024), ("small_0_200KiB", small)):
+        d = tempfile.mkdtemp(prefix="sf_sw_")
+        try:
+            paths = write_tree(d, lens, 5)
+            for S in ss:
+                for io in ios:
+                    for j in js:
+                        env = dict(os.environ, SF_IO_THREADS=str(io))
+                        r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-j", str(j), "-S", str(S)] + paths,
+                                           capture_output=True, text=True, env=env, timeout=300)
+                        if r.returncode:
+                            print(json.dumps({"tree": name, "error": r.stderr[-300:]}), flush=True)
+                            return 1
+                        t = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")][-1]
+                        print(json.dumps({"tree": name, "j": j, "io": io, "S": S,
+                                          "GB/s": round(t["bytes"] / t["wall_s"] / 1e9, 3),
+                                          "wall": round(t["wall_s"], 3), "hash": round(t["hash_call_s"], 3),
+                                          "wait": round(t["wait_cut_s"], 3), "chunk_cpu": round(t["chunk_cpu_s"], 2),
+                                          "open": round(t["open_s"], 2), "read": round(t["read_s"], 2)}),
+                              flush=True)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

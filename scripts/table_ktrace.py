@@ -4,7 +4,9 @@ rocprofv3 --kernel-trace (no counters): the dispatch order is cdc_ab.py's
 sha1_table_kernel launch is attributed to its library and list, with the
 sort kernels before it and the gaps around it.
 usage: python scripts/table_ktrace.py kernel_trace.csv LISTS NLIBS REPS ROUNDS [rot]
-(rot: cdc_ab.py rotated the library order every round, its default since s22)"""
+(rot: cdc_ab.py rotated the library order every round, its default since s22).
+A library whose sort ends with group_geo_kernel (round 5) counts it in the
+sort's time."""
 import csv
 import statistics
 import sys
@@ -22,9 +24,9 @@ def main():
             fixed.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
         if "class_hist_kernel" in n:
             cur = [r]
-        elif cur and ("class_scan" in n or "class_scatter" in n):
+        elif cur and ("class_scan" in n or "class_scatter" in n or "group_geo" in n):
             cur.append(r)
-        elif "sha1_table_kernel<128, false>" in n and len(cur) == 3:
+        elif "sha1_table_kernel<128, false>" in n and len(cur) in (3, 4):
             cur.append(r)
             calls.append(cur)
             cur = []
@@ -41,8 +43,8 @@ def main():
                     c = calls[i]
                     i += 1
                     t = [(int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in c]
-                    res.setdefault((lib, k), []).append(((t[3][1] - t[3][0]) / 1e3, (t[3][0] - t[0][0]) / 1e3,
-                                                          (t[3][1] - t[0][0]) / 1e3))
+                    res.setdefault((lib, k), []).append(((t[-1][1] - t[-1][0]) / 1e3, (t[-1][0] - t[0][0]) / 1e3,
+                                                          (t[-1][1] - t[0][0]) / 1e3))
     if fixed:
         print(f"fixed kernel median {statistics.median(fixed):.1f} us ({len(fixed)} launches)")
     for (lib, k), v in sorted(res.items()):

@@ -641,10 +641,13 @@ static int index_stream(int fd, uint32_t bs, RowBuf& rows, uint8_t* blocks_hash)
 // the disk while stage k is copied; for a resident file both are no-ops.
 inline bool fadvise_on() { return knob(K_FADVISE) != 0; }
 
+}  // namespace
+
+namespace sfi {
+
 // Bytes [base, base + len) of the file (base a multiple of bs: a shard of
 // one logical file); row offsets are file offsets.
-static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf_block_sig* out,
-                            uint8_t* blocks_hash) {
+int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf_block_sig* out, uint8_t* blocks_hash) {
   const unsigned nthreads = std::max(1u, std::min(io_threads(), std::thread::hardware_concurrency()));
   const bool adv = fadvise_on();
   if (adv) (void)posix_fadvise(fd, (off_t)base, (off_t)len, POSIX_FADV_SEQUENTIAL);
@@ -683,6 +686,10 @@ static int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf
   };
   return staged_pipeline(bs, file_stage_bytes(bs), fill, emit, blocks_hash);
 }
+
+}  // namespace sfi
+
+namespace {
 
 // Copy n bytes into a pinned stage with several threads (one thread moves
 // ~10-16 GB/s, below the PCIe link the stage is waiting for).

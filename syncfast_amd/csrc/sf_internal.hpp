@@ -45,7 +45,7 @@ namespace sfi __attribute__((visibility("hidden"))) {
 enum Knob {
   K_IO_THREADS, K_INPLACE_MIN_MIB, K_INPLACE_SERIAL, K_FADVISE, K_NO_HOSTREG, K_TABLE_CLASS_BITS, K_TRACE,
   K_TEST_INPLACE_FAIL_AT, K_TEST_WIRE_CHUNK, K_TEST_STREAM_STAGE_MIB, K_TEST_LAUNCH_MAX_BLOCKS, K_TEST_TABLE_SORT,
-  K_TEST_CHAIN_SPIN_LIMIT, K_TEST_STAGES, K_COUNT
+  K_TEST_CHAIN_SPIN_LIMIT, K_TEST_STAGES, K_TEST_MULTI_SELF_GATHER, K_COUNT
 };
 struct KnobDef {
   const char* env;
@@ -262,6 +262,12 @@ class HostLease {
 bool stamp_of(int fd, sf_file_stamp* s, mode_t* mode);
 bool same_stamp(const sf_file_stamp& a, const sf_file_stamp& b);
 
+// Fixed tiling of bytes [base, base + len) of the regular file open on fd
+// (base a multiple of bs) through the staged pread pipeline (sf_host.cpp) on
+// the calling thread's current device: rows (file offsets) into out[0, ...),
+// blocks_hash (may be NULL) over this range's digests.  A short read is SF_EIO.
+int index_file_pread(int fd, uint64_t base, uint64_t len, uint32_t bs, sf_block_sig* out, uint8_t* blocks_hash);
+
 // Reader threads of the pread routes (sf_index_file, sf_index_files).
 // SF_IO_THREADS overrides the default of 16 (A/B knob, latched at load).  With the stat phase
 // parallel too, 16 readers beat 8 on many small files (10,537 files of
@@ -280,11 +286,19 @@ inline unsigned io_threads() {
 size_t class_order_workspace(uint64_t n, uint32_t kmax);
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
                 hipStream_t s);
+// The sorted list's blocks in processing order -- d_soff / d_ssz, their
+// offsets and sizes -- and every group of 64's geometry (d_gtab, one 32-B
+// sf::GroupGeo per group), stream-ordered on s (sf_sort.hip).
+constexpr size_t kGroupGeoBytes = 32;
+int group_geometry(const uint32_t* d_order, const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t len,
+                   uint64_t n, uint64_t* d_soff, uint32_t* d_ssz, void* d_gtab, hipStream_t s);
 // sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
-// translation unit), one group of 64 blocks per wave; SF_OK or the launch
-// error.
+// translation unit), one group of 64 blocks per wave; a sorted launch passes
+// order, soff, ssz and gtab (group_geometry), an unsorted one NULLs.  SF_OK
+// or the launch error.
 int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, const uint64_t* d_offsets,
                         const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests, int* d_status, uint32_t* weak,
-                        const uint32_t* order, hipStream_t stream);
+                        const uint32_t* order, const uint64_t* soff, const uint32_t* ssz, const void* gtab,
+                        hipStream_t stream);
 
 }  // namespace sfi

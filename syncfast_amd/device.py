@@ -26,7 +26,7 @@ from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
 __all__ = [
     "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
     "index_device_weak", "index_device_blocks_weak", "BatchStream",
-    "fill_splitmix", "splitmix_tensor", "BlockSet",
+    "fill_splitmix", "splitmix_tensor", "BlockSet", "index_device_multi",
 ]
 
 
@@ -425,6 +425,41 @@ class BlockSet:
             self.close()
         except Exception:
             pass
+
+
+def index_device_multi(shards: Sequence[torch.Tensor], file_len: int, block_size: int, root: int = 0,
+                       table: Optional[torch.Tensor] = None, scratch: Optional[Sequence[torch.Tensor]] = None,
+                       streams: Optional[Sequence[torch.cuda.Stream]] = None) -> torch.Tensor:
+    """sf_index_device_multi: shards[r] (on cuda:r) holds shard r
+    (host.shard_range) of one logical file; every shard is hashed on its own
+    device and the digest tables meet in `table` on cuda:root, gathered over
+    xGMI with RCCL inside the library.  Returns the (nblocks, 20) table,
+    complete once root's stream has run past the call."""
+    n = len(shards)
+    if n < 1:
+        raise ValueError("no shards")
+    from .host import shard_range
+    nb = num_blocks(file_len, block_size)
+    for r, t in enumerate(shards):
+        _require_device(t, f"shards[{r}]", torch.uint8, torch.device("cuda", r))
+        if t.numel() != shard_range(file_len, block_size, n, r)[1]:
+            raise ValueError(f"shards[{r}] is not shard {r} of {n}")
+    dev_root = torch.device("cuda", root)
+    if table is None:
+        table = torch.empty((max(nb, 1), 20), dtype=torch.uint8, device=dev_root)
+    _require_device(table, "table", torch.uint8, dev_root)
+    if table.numel() < nb * 20:
+        raise ValueError("table too small")
+    if scratch is None:
+        scratch = [torch.empty((max(num_blocks(t.numel(), block_size), 1), 20), dtype=torch.uint8, device=t.device)
+                   for t in shards]
+    ptr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+    sp = None
+    if streams is not None:
+        sp = (ctypes.c_void_p * n)(*[s.cuda_stream for s in streams])
+    check(lib().sf_index_device_multi(n, ptr(shards), file_len, block_size, ptr(scratch), root, table.data_ptr(), sp),
+          "sf_index_device_multi")
+    return table[:nb]
 
 
 def fill_splitmix(out: torch.Tensor, seed: int, start: int = 0,

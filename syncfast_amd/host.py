@@ -261,6 +261,36 @@ def index_fds_blocks(fds: Sequence[int], lists: Sequence[Tuple[object, object]],
     return out[:total], first, hashes[:n], status[:n]
 
 
+def shard_range(file_len: int, block_size: int, n_shards: int, shard: int) -> Tuple[int, int]:
+    """sf_shard_range: (start, length) of shard `shard` of n_shards (the
+    partition of the multi-device forms)."""
+    s, n = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().sf_shard_range(file_len, block_size, n_shards, shard, ctypes.byref(s), ctypes.byref(n)),
+          "sf_shard_range")
+    return s.value, n.value
+
+
+def index_file_multi(path, block_size: int, n_devices: int = 0) -> Tuple[np.ndarray, bytes]:
+    """One regular file on N devices of this process (sf_index_file_multi):
+    shard r read and hashed on device r by a host thread of its own, rows in
+    file order, blocks_hash over all digests.  n_devices = 0: every visible
+    device."""
+    size = os.stat(path).st_size
+    n = (size + block_size - 1) // block_size if size else 0
+    need = ctypes.c_uint64(0)
+    bh = (ctypes.c_uint8 * 20)()
+    for _attempt in range(4):  # the file may grow between the stat and the call
+        out = np.zeros(max(n, 1), SIG_DTYPE)
+        rc = lib().sf_index_file_multi(os.fsencode(path), block_size, n_devices,
+                                       out.ctypes.data_as(ctypes.POINTER(BlockSig)), n, ctypes.byref(need), bh)
+        if rc == SF_ENOSPC and need.value > n:
+            n = need.value
+            continue
+        break
+    check(rc, f"sf_index_file_multi({os.fsdecode(path)})")
+    return out[:need.value], bytes(bh)
+
+
 def blocks_hash(digests) -> bytes:
     """compute_blocks_hash: SHA-1 over the 20-byte digests in order."""
     d = _u8(digests)

@@ -13,6 +13,7 @@ over RCCL on MI355X and over gloo in the CPU tests.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Tuple
 
 import torch
@@ -191,13 +192,22 @@ def index_file_sharded(path, block_size: int, group: Optional[dist.ProcessGroup]
 
 
 def index_file_blocks_sharded(path, offsets, sizes, group: Optional[dist.ProcessGroup] = None, dst: int = 0,
-                              device: Optional[torch.device] = None):
+                              device: Optional[torch.device] = None, stamp=None):
     """The reference's default (content-defined) blocks of one file on N
     ranks: every rank holds the same offset-ordered list (the host chunker's
     output over the file, src/index.rs:622-625), takes its list_shards range
-    and hashes those blocks from the file on its own GPU
-    (sf_index_file_blocks); the digests are gathered to `dst`, which returns
-    the file's rows in list order and its blocks_hash (src/index.rs:661-682).
+    and hashes those blocks from the file on its own GPU; the digests are
+    gathered to `dst`, which returns the file's rows in list order and its
+    blocks_hash (src/index.rs:661-682).
+
+    One version of the file: `stamp` (on `dst`, host.file_stamp of the
+    descriptor the chunker read, taken before it read) is broadcast, and
+    every rank hashes its blocks from its own open of the path through
+    sf_index_fd_blocks with that stamp as the expected one -- a file renamed
+    over the path or written after the chunker's stamp gives SF_EAGAIN on the
+    rank that sees it, and then on every rank, so the caller cuts the file
+    again; the gathered table never mixes two versions.  Without a stamp each
+    rank stamps its own open (the call still fails on a change during it).
     The ranks agree on success before the gather, as index_file_sharded does.
     Returns (rows, blocks_hash) on `dst`, None elsewhere."""
     import os
@@ -205,24 +215,43 @@ def index_file_blocks_sharded(path, offsets, sizes, group: Optional[dist.Process
     import numpy as np
 
     from . import host
-    from ._lib import SF_EIO, SfError
+    from ._lib import SF_EAGAIN, SF_EIO, FileStamp, SfError
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     is_dst = dist.get_rank() == dst
     where = device if device is not None else torch.device("cpu")
     offs = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
     szs = np.ascontiguousarray(sizes, dtype=np.uint32).reshape(-1)
+    # dst's stamp to every rank (dev, ino, size, nlink, mtime, ctime; all -1: none)
+    fields = [f for f, _t in FileStamp._fields_]
+    st_t = torch.full((len(fields),), -1, dtype=torch.int64, device=where)
+    if is_dst and stamp is not None:
+        st_t = torch.tensor([ctypes.c_int64(int(getattr(stamp, f))).value for f in fields], dtype=torch.int64,
+                            device=where)  # uint64 fields carried bit for bit
+    dist.broadcast(st_t, src=dst, group=group)
+    vals = st_t.cpu().tolist()
+    expect = None
+    if any(v != -1 for v in vals):
+        expect = FileStamp(*[v & 0xFFFFFFFFFFFFFFFF if t is not ctypes.c_int64 else v
+                             for v, (_f, t) in zip(vals, FileStamp._fields_)])
     cuts = list_shards(offs, szs, world)
     b0, b1 = cuts[rank], cuts[rank + 1]
     failure: Optional[BaseException] = None
     try:
-        rows, _ = host.index_file_blocks(path, offs[b0:b1], szs[b0:b1])
+        fd = os.open(path, os.O_RDONLY | os.O_NONBLOCK)
+        try:
+            rows, _ = host.index_fd_blocks(fd, offs[b0:b1], szs[b0:b1], expect)
+        finally:
+            os.close(fd)
     except (SfError, OSError, ValueError) as e:
         failure = e
-    failed = torch.tensor([1 if failure is not None else 0], dtype=torch.int32, device=where)
+    code = 0 if failure is None else (2 if isinstance(failure, SfError) and failure.code == SF_EAGAIN else 1)
+    failed = torch.tensor([code], dtype=torch.int32, device=where)
     dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=group)
     if failure is not None:
         raise failure
+    if int(failed.item()) == 2:
+        raise SfError(SF_EAGAIN, f"index_file_blocks_sharded: {os.fsdecode(path)} changed under another rank")
     if int(failed.item()):
         raise SfError(SF_EIO, f"index_file_blocks_sharded: another rank failed on {os.fsdecode(path)}")
     dig = torch.from_numpy(np.ascontiguousarray(rows["sha1"]).reshape(-1, 20))

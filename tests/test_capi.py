@@ -525,3 +525,51 @@ def test_fds_blocks_checks_before_any_device_call(tmp_path):
             f.close()
         os.close(r)
         os.close(w)
+
+
+def test_shard_range_c_equals_python():
+    """sf_shard_range (the multi-device forms' partition) is
+    syncfast_amd.shard.shard_range, the one-process-per-GPU partition."""
+    from syncfast_amd.shard import shard_range
+    L = syncfast_amd.lib()
+    s, n = ctypes.c_uint64(), ctypes.c_uint64()
+    rng = np.random.default_rng(3)
+    cases = [(0, 4096, 1), (1, 4096, 8), (4096 * 8, 4096, 8), (4096 * 8 + 1, 4096, 8), (10, 3, 7), (7, 100, 3)]
+    cases += [(int(rng.integers(0, 1 << 40)), int(rng.integers(1, 1 << 20)), int(rng.integers(1, 9)))
+              for _ in range(200)]
+    for total, bs, world in cases:
+        prev_end = 0
+        for r in range(world):
+            assert L.sf_shard_range(total, bs, world, r, ctypes.byref(s), ctypes.byref(n)) == 0
+            assert (s.value, n.value) == shard_range(total, bs, world, r)
+            assert s.value == prev_end or n.value == 0
+            prev_end = s.value + n.value if n.value else prev_end
+        assert prev_end == total
+    assert L.sf_shard_range(100, 0, 2, 0, ctypes.byref(s), ctypes.byref(n)) == _lib.SF_EINVAL
+    assert L.sf_shard_range(100, 10, 0, 0, ctypes.byref(s), ctypes.byref(n)) == _lib.SF_EINVAL
+    assert L.sf_shard_range(100, 10, 2, 2, ctypes.byref(s), ctypes.byref(n)) == _lib.SF_EINVAL
+    assert L.sf_shard_range(100, 10, 2, 0, None, ctypes.byref(n)) == _lib.SF_EINVAL
+
+
+def test_multi_device_argument_checks(tmp_path):
+    """The multi-device forms check their arguments before touching a device
+    (on this machine, with no device, a valid call is SF_ENODEV)."""
+    L = syncfast_amd.lib()
+    p = tmp_path / "f"
+    p.write_bytes(b"x" * 10000)
+    out = np.zeros(4, host.SIG_DTYPE)
+    sig = out.ctypes.data_as(ctypes.POINTER(_lib.BlockSig))
+    need = ctypes.c_uint64()
+    bh = (ctypes.c_uint8 * 20)()
+    assert L.sf_index_file_multi(os.fsencode(p), 0, 1, sig, 4, ctypes.byref(need), bh) == _lib.SF_EINVAL
+    assert L.sf_index_file_multi(os.fsencode(p), (32 << 20) + 1, 1, sig, 4, ctypes.byref(need), bh) == _lib.SF_EINVAL
+    assert L.sf_index_file_multi(None, 4096, 1, sig, 4, ctypes.byref(need), bh) == _lib.SF_EINVAL
+    assert L.sf_index_file_multi(os.fsencode(p), 4096, 1, sig, 4, ctypes.byref(need), None) == _lib.SF_EINVAL
+    one = (ctypes.c_void_p * 1)(1)
+    assert L.sf_index_device_multi(0, one, 100, 4096, one, 0, 1, None) == _lib.SF_EINVAL
+    assert L.sf_index_device_multi(1, one, 100, 4096, one, 1, 1, None) == _lib.SF_EINVAL  # root out of range
+    assert L.sf_index_device_multi(1, None, 100, 4096, one, 0, 1, None) == _lib.SF_EINVAL
+    assert L.sf_index_device_multi(1, one, 100, 0, one, 0, 1, None) == _lib.SF_EINVAL
+    if _lib.device_count() == 0:
+        assert L.sf_index_file_multi(os.fsencode(p), 4096, 1, sig, 4, ctypes.byref(need), bh) == _lib.SF_ENODEV
+        assert L.sf_index_device_multi(1, one, 100, 4096, one, 0, 1, None) == _lib.SF_ENODEV

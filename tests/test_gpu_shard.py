@@ -199,15 +199,32 @@ def test_rccl_gather_path_world1(gpu):
     assert got == oracle.index_fixed(oracle.splitmix_bytes(n, 0x5EED0008), bs)[2].tobytes()
 
 
-def _list_rank(rank, world, port, path, offs, sizes, q):
+def _list_rank(rank, world, port, path, offs, sizes, q, stale=False):
+    import time
+
     import torch.distributed as dist
 
+    from syncfast_amd import _lib, host
     from syncfast_amd.shard import index_file_blocks_sharded
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = index_file_blocks_sharded(path, offs, sizes)
+        stamp = None
+        if rank == 0:  # the chunking rank: its stamp, taken before the chunker read the file
+            with open(path, "rb") as f:
+                stamp = host.file_stamp(f.fileno())
+            if stale:  # written after the chunker's stamp: no rank may hash it under that list
+                time.sleep(0.02)
+                with open(path, "r+b") as g:
+                    g.seek(12345)
+                    g.write(b"\x77" * 100)
+        dist.barrier()
+        try:
+            res = index_file_blocks_sharded(path, offs, sizes, stamp=stamp)
+        except _lib.SfError as e:
+            q.put(("error", e.code, rank))
+            return
         if rank == 0:
             rows, bh = res
             q.put((rows.tobytes(), bh))
@@ -215,6 +232,30 @@ def _list_rank(rank, world, port, path, offs, sizes, q):
             assert res is None
     finally:
         dist.destroy_process_group()
+
+
+def test_hip_list_shards_stale_stamp_fails_every_rank(gpu, tmp_path):
+    """the chunking rank's stamp is broadcast; a file written after
+    it is SF_EAGAIN on every rank (the caller cuts it again), never a gathered
+    table that mixes two versions."""
+    import torch.multiprocessing as mp
+    n = (8 << 20) + 3
+    path = tmp_path / "cdc.bin"
+    oracle.splitmix_bytes(n, 0x5EED0300).tofile(path)
+    b = np.arange(0, n, 8000, dtype=np.uint64)
+    offs, szs = b, np.diff(np.concatenate([b, [n]])).astype(np.uint32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_list_rank, args=(r, 2, port, str(path), offs, szs, q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=100) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from syncfast_amd import _lib
+    assert sorted(g[2] for g in got) == [0, 1] and all(g[0] == "error" and g[1] == _lib.SF_EAGAIN for g in got)
 
 
 @pytest.mark.parametrize("world", [2, 3])
