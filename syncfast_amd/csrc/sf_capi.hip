@@ -119,7 +119,7 @@ inline uint64_t table_sort_min() {
   if (v >= 0) return v ? 1 : ~0ull;
   return 1ull << 17;
 }
-constexpr uint64_t kSortMaxBlocks = 1ull << 26;  // blocks per sorted piece (~1.1 GiB of workspace at most)
+constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
 
 // Stream-ordered workspace holding the processing order of blocks [0, n) of
 // a list: stable sort of the blocks by length class, descending, on `s`
@@ -130,24 +130,13 @@ constexpr uint64_t kSortMaxBlocks = 1ull << 26;  // blocks per sorted piece (~1.
 // The key takes the counting sort of sf_sort.hip (three kernels, ~21 us for
 // 0.5 M blocks with the default 8-bit key, against ~56 us of GPU time for
 // rocprim's radix sort with its key kernel; profiles/r03/sort/), the 9- and
-// 10-bit keys of the SF_TABLE_CLASS_BITS knob too (512 / 1024 bins).  After
-// the sort, group_geometry lays the blocks' offsets and sizes out in that
-// order and writes every group's geometry, so a wave of the table kernel
-// starts with independent loads and one scalar load (round 5).
-struct TableOrder {
-  void* ws = nullptr;         // stream-ordered workspace holding the rest (hipFreeAsync after the launch)
-  uint32_t* order = nullptr;  // processing order (block indices)
-  uint64_t* soff = nullptr;   // the blocks' offsets in that order
-  uint32_t* ssz = nullptr;    // their sizes
-  void* gtab = nullptr;       // every group of 64's geometry (sf::GroupGeo)
-};
-
-// The sort and the group geometry of a list of n blocks on `s`; false (an
-// unsorted launch) if anything fails.
-bool table_order(const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t len, uint64_t n, hipStream_t s,
-                 TableOrder* t) {
+// 10-bit keys of the SF_TABLE_CLASS_BITS knob too (512 / 1024 bins).
+// Returns nullptr (unsorted launch) if anything fails.
+uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void** ws_out) {
+  *ws_out = nullptr;
   // mantissa bits of the length class, 1..6 (SF_TABLE_CLASS_BITS, A/B knob)
   const uint32_t mbits = (uint32_t)std::min<int64_t>(6, std::max<int64_t>(1, knob(K_TABLE_CLASS_BITS)));
+
   // classes < 32 << mbits; the key is clamped at (16 << mbits) - 1, so every
   // block of 2^16+ compressions (>= 4 MiB) shares the top class: 8 bits with
   // 4 mantissa bits (the default; class width 6.25 %), 9 with 5, 10 with 6
@@ -155,26 +144,21 @@ bool table_order(const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t le
   const unsigned kbits = mbits <= 4 ? 8u : 4u + mbits;
   const uint32_t kmax = (1u << kbits) - 1u;
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t ob = up(n * 4), cb = up(class_order_workspace(n, kmax)), sb = up(n * 8), zb = up(n * 4);
-  const size_t gb = up(ceil_div(n, 64) * kGroupGeoBytes);
+  // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
+  const size_t ob = up(n * 4), total = ob + up(sfi::class_order_workspace(n, kmax));
   uint8_t* ws = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&ws), ob + cb + sb + zb + gb, s) != hipSuccess) {
+  if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
     (void)hipGetLastError();
-    return false;
+    return nullptr;
   }
-  t->ws = ws;
-  t->order = reinterpret_cast<uint32_t*>(ws);
-  t->soff = reinterpret_cast<uint64_t*>(ws + ob + cb);
-  t->ssz = reinterpret_cast<uint32_t*>(ws + ob + cb + sb);
-  t->gtab = ws + ob + cb + sb + zb;
-  if (class_order(d_sizes, n, mbits, kmax, ws + ob, t->order, s) != SF_OK ||
-      group_geometry(t->order, d_offsets, d_sizes, len, n, t->soff, t->ssz, t->gtab, s) != SF_OK) {
+  uint32_t* order = reinterpret_cast<uint32_t*>(ws);
+  if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, s) != SF_OK) {
     (void)hipGetLastError();
     (void)hipFreeAsync(ws, s);
-    *t = TableOrder{};
-    return false;
+    return nullptr;
   }
-  return true;
+  *ws_out = ws;
+  return order;
 }
 
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
@@ -191,12 +175,11 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
     }
     return SF_OK;
   }
-  TableOrder t;
-  if (sorted) (void)table_order(d_offsets, d_sizes, len, nblocks, stream, &t);
+  void* ws = nullptr;
+  const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
   const int rc = launch_table_kernel(weak != nullptr, static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes,
-                                     nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, t.order, t.soff, t.ssz,
-                                     t.gtab, stream);
-  if (t.ws) (void)hipFreeAsync(t.ws, stream);
+                                     nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order, stream);
+  if (ws) (void)hipFreeAsync(ws, stream);
   return rc;
 }
 

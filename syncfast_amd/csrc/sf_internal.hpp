@@ -286,19 +286,11 @@ inline unsigned io_threads() {
 size_t class_order_workspace(uint64_t n, uint32_t kmax);
 int class_order(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, void* d_ws, uint32_t* d_order,
                 hipStream_t s);
-// The sorted list's blocks in processing order -- d_soff / d_ssz, their
-// offsets and sizes -- and every group of 64's geometry (d_gtab, one 32-B
-// sf::GroupGeo per group), stream-ordered on s (sf_sort.hip).
-constexpr size_t kGroupGeoBytes = 32;
-int group_geometry(const uint32_t* d_order, const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t len,
-                   uint64_t n, uint64_t* d_soff, uint32_t* d_ssz, void* d_gtab, hipStream_t s);
 // sha1_table_kernel<128, weak_form> on `stream` (sf_table.hip, its own
-// translation unit), one group of 64 blocks per wave; a sorted launch passes
-// order, soff, ssz and gtab (group_geometry), an unsorted one NULLs.  SF_OK
-// or the launch error.
+// translation unit), one group of 64 blocks per wave; SF_OK or the launch
+// error.
 int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, const uint64_t* d_offsets,
                         const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests, int* d_status, uint32_t* weak,
-                        const uint32_t* order, const uint64_t* soff, const uint32_t* ssz, const void* gtab,
-                        hipStream_t stream);
+                        const uint32_t* order, hipStream_t stream);
 
 }  // namespace sfi

@@ -764,18 +764,6 @@ constexpr int kTableWG = 4;             // its waves per workgroup
 constexpr uint32_t kTableRound = 1024u; // waves per dispatch round: MI355X's SIMDs (256 CUs x 4)
 constexpr uint32_t kTableReversedRounds = 2u;  // bit r: round r takes its groups in reverse (round 1 only)
 
-// The geometry of one group of 64 blocks of a sorted explicit list, written
-// by the sort (sf_sort.hip, group_geo_kernel) beside the blocks' offsets and
-// sizes in processing order, so that a wave of sha1_table_kernel reads it
-// with one scalar load instead of reducing it over its lanes after two
-// dependent loads (order -> offsets / sizes).  Out-of-range blocks count as
-// empty blocks at offset 0, as in the kernel.
-struct GroupGeo {
-  uint64_t lo, hi;                       // the group's lowest block start, highest block end
-  uint32_t min_size, max_size, max_nch;  // over its blocks
-  uint32_t aligned;                      // every block 16-B aligned
-};
-
 // Explicit block list: block i = data[offsets[i], offsets[i] + sizes[i]).
 // Used for content-defined boundaries, the reference KAT boundaries, ragged
 // many-file batches, and (over the digest table) per-file blocks_hash.
@@ -783,64 +771,40 @@ struct GroupGeo {
 // set to -34 (SF_ERANGE).
 // Group g of the list = 64 blocks, one lane each: order[64g .. 64g + 63] when
 // the launcher sorted the list (each digest is written at the block's own
-// index; the blocks' offsets and sizes in that order are soff / ssz, the
-// group's geometry gtab[g]), else blocks 64g .. 64g + 63.
+// index), else blocks 64g .. 64g + 63.
 template <int TILE, bool WEAK>
 __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, uint64_t len,
                                             const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ sizes,
                                             uint64_t nblocks, uint8_t* __restrict__ digests, int* __restrict__ status,
                                             uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
-                                            const uint64_t* __restrict__ soff, const uint32_t* __restrict__ ssz,
-                                            const GroupGeo* __restrict__ gtab, uint64_t g, uint4* __restrict__ tile) {
+                                            uint64_t g, uint4* __restrict__ tile) {
   const int lane = lane_id();
   const uint64_t first = g * 64;
   bool valid = first + lane < nblocks;
-  uint64_t blk = first + lane;
+  const uint64_t blk = (order && valid) ? (uint64_t)order[first + lane] : first + lane;
   uint64_t off = 0;
   uint32_t size = 0;
   bool bad = false;
-  WaveGeo geo;
-  uint64_t lo, hi;
-  if (order) {
-    // sorted: three independent loads per lane and one scalar load per wave
-    const GroupGeo d = gtab[g];
-    if (valid) {
-      blk = order[first + lane];
-      off = soff[first + lane];
-      size = ssz[first + lane];
-      if (off > len || (uint64_t)size > len - off) {
-        bad = true;
-        off = 0;
-        size = 0;
-      }
+  if (valid) {
+    off = offsets[blk];
+    size = sizes[blk];
+    if (off > len || (uint64_t)size > len - off) {
+      bad = true;
+      off = 0;
+      size = 0;
     }
-    lo = d.lo;
-    hi = d.hi;
-    geo.min_size = d.min_size;
-    geo.max_size = d.max_size;
-    geo.max_nch = d.max_nch;
-    geo.lds_ok = d.aligned != 0;
-  } else {
-    if (valid) {
-      off = offsets[blk];
-      size = sizes[blk];
-      if (off > len || (uint64_t)size > len - off) {
-        bad = true;
-        off = 0;
-        size = 0;
-      }
-    }
-    lo = wave_min_u64(valid ? off : ~0ull);
-    hi = wave_max_u64(valid ? off + size : 0ull);
-    geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
-    geo.max_size = wave_max_u32(valid ? size : 0u);
-    geo.max_nch = wave_max_u32(valid ? n_chunks_wide(size) : 0u);
-    const bool aligned = !valid || ((off & 15u) == 0);
-    geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned));
   }
+  WaveGeo geo;
+  const uint64_t lo = wave_min_u64(valid ? off : ~0ull);
+  const uint64_t hi = wave_max_u64(valid ? off + size : 0ull);
   geo.base = lo;
   geo.span = hi - lo;
-  geo.lds_ok = geo.lds_ok && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
+  geo.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
+  geo.max_size = wave_max_u32(valid ? size : 0u);
+  geo.max_nch = wave_max_u32(valid ? n_chunks_wide(size) : 0u);
+  const bool aligned = !valid || ((off & 15u) == 0);
+  geo.lds_ok = __builtin_amdgcn_readfirstlane(__all(aligned)) &&
+               ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) && geo.span < 0xF0000000ull;
   const uint32_t rel = valid ? (uint32_t)(off - lo) : 0u;
 
   Sha1 st;
@@ -889,20 +853,20 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
 //     the sort's order the same SIMDs would start with every round's
 //     longest group.  Round 1 therefore takes its groups in reverse (below):
 //     SIMD work max/mean 1.07 -> 1.047, the CDC-like list 2 % faster.
-// Sorted launches (order != NULL) also pass the blocks' offsets and sizes in
-// processing order (soff, ssz) and every group's geometry (gtab).
+// next_group: unused (kept in the signature until the list kernel's next
+// form replaces it).
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(64 * kTableWG, kTableWavesPerSimd)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
                   int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
-                  const uint64_t* __restrict__ soff, const uint32_t* __restrict__ ssz,
-                  const GroupGeo* __restrict__ gtab) {
+                  uint32_t* __restrict__ next_group) {
   constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
   __shared__ uint4 smem[kTableWG * kWaveTile];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint4* tile = smem + wid * kWaveTile;
   const uint32_t ngroups = (uint32_t)((nblocks + 63) / 64);  // <= 2^25: the launcher splits at 2^31 blocks
+  (void)next_group;
   uint32_t g = blockIdx.x * kTableWG + wid;
   // The first rounds of waves land one per SIMD per round (wave w and
   // w + kTableRound on the same SIMD, traces of round 4), so in the sort's
@@ -918,8 +882,7 @@ sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t
     const uint32_t R = kTableRound, r = g / R;
     if (r < 8 && ((kTableReversedRounds >> r) & 1u) && (r + 1) * R <= ngroups) g = r * R + (R - 1u - g % R);
   }
-  if (g < ngroups)
-    table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, soff, ssz, gtab, g, tile);
+  if (g < ngroups) table_group<TILE, WEAK>(data, len, offsets, sizes, nblocks, digests, status, weak, order, g, tile);
 }
 
 // The length class of a block for sha1_table_kernel's `order` (sf_sort.hip's

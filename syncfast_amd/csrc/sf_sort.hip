@@ -164,57 +164,9 @@ class_scatter_kernel(const uint32_t* __restrict__ sizes, uint64_t n, uint32_t mb
   }
 }
 
-// 4. Every group of 64 blocks in processing order: the blocks' offsets and
-// sizes in that order (soff, ssz) and the group's geometry (gtab), one wave
-// per group -- what sha1_table_kernel's waves would otherwise reduce over
-// their lanes after two dependent loads.  An out-of-range block counts as an
-// empty block at offset 0, as in the kernel.
-__global__ void __launch_bounds__(kSortThreads)
-group_geo_kernel(const uint32_t* __restrict__ order, const uint64_t* __restrict__ offsets,
-                 const uint32_t* __restrict__ sizes, uint64_t len, uint64_t n, uint64_t* __restrict__ soff,
-                 uint32_t* __restrict__ ssz, GroupGeo* __restrict__ gtab) {
-  const uint64_t g = ((uint64_t)blockIdx.x * kSortThreads + threadIdx.x) / 64;
-  const int lane = threadIdx.x & 63;
-  const uint64_t i = g * 64 + lane;
-  if (g * 64 >= n) return;
-  const bool valid = i < n;
-  uint64_t off = 0;
-  uint32_t size = 0;
-  if (valid) {
-    const uint32_t blk = order[i];
-    off = offsets[blk];
-    size = sizes[blk];
-    soff[i] = off;
-    ssz[i] = size;
-    if (off > len || (uint64_t)size > len - off) {
-      off = 0;
-      size = 0;
-    }
-  }
-  GroupGeo d;
-  d.lo = wave_min_u64(valid ? off : ~0ull);
-  d.hi = wave_max_u64(valid ? off + size : 0ull);
-  d.min_size = wave_min_u32(valid ? size : 0xFFFFFFFFu);
-  d.max_size = wave_max_u32(valid ? size : 0u);
-  d.max_nch = wave_max_u32(valid ? n_chunks_wide(size) : 0u);
-  d.aligned = __builtin_amdgcn_readfirstlane(__all(!valid || (off & 15u) == 0)) ? 1u : 0u;
-  if (lane == 0) gtab[g] = d;
-}
-
 }  // namespace sf
 
 namespace sfi {
-
-int group_geometry(const uint32_t* d_order, const uint64_t* d_offsets, const uint32_t* d_sizes, uint64_t len,
-                   uint64_t n, uint64_t* d_soff, uint32_t* d_ssz, void* d_gtab, hipStream_t s) {
-  static_assert(sizeof(sf::GroupGeo) == kGroupGeoBytes, "GroupGeo layout");
-  if (n == 0) return SF_OK;
-  const uint64_t groups = (n + 63) / 64;
-  hipLaunchKernelGGL(sf::group_geo_kernel, dim3((unsigned)ceil_div(groups, sf::kSortThreads / 64)),
-                     dim3(sf::kSortThreads), 0, s, d_order, d_offsets, d_sizes, len, n, d_soff, d_ssz,
-                     static_cast<sf::GroupGeo*>(d_gtab));
-  return hip_err(hipGetLastError());
-}
 
 static uint32_t sort_bins(uint32_t kmax) { return kmax < 256 ? 256u : kmax < 512 ? 512u : 1024u; }
 

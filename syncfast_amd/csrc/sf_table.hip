@@ -15,17 +15,16 @@ namespace sfi {
 
 int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, const uint64_t* d_offsets,
                         const uint32_t* d_sizes, uint64_t nblocks, uint8_t* d_digests, int* d_status, uint32_t* weak,
-                        const uint32_t* order, const uint64_t* soff, const uint32_t* ssz, const void* gtab,
-                        hipStream_t stream) {
+                        const uint32_t* order, hipStream_t stream) {
   const uint64_t ngroups = (nblocks + 63) / 64;
   const unsigned grid = (unsigned)((ngroups + sf::kTableWG - 1) / sf::kTableWG);
-  const sf::GroupGeo* g = static_cast<const sf::GroupGeo*>(gtab);
+  uint32_t* const next_group = nullptr;
   if (weak_form)
     hipLaunchKernelGGL((sf::sha1_table_kernel<128, true>), dim3(grid), dim3(64 * sf::kTableWG), 0, stream, d_data, len,
-                       d_offsets, d_sizes, nblocks, d_digests, d_status, weak, order, soff, ssz, g);
+                       d_offsets, d_sizes, nblocks, d_digests, d_status, weak, order, next_group);
   else
     hipLaunchKernelGGL((sf::sha1_table_kernel<128, false>), dim3(grid), dim3(64 * sf::kTableWG), 0, stream, d_data, len,
-                       d_offsets, d_sizes, nblocks, d_digests, d_status, nullptr, order, soff, ssz, g);
+                       d_offsets, d_sizes, nblocks, d_digests, d_status, nullptr, order, next_group);
   return hip_err(hipGetLastError());
 }
 

@@ -573,3 +573,16 @@ def test_multi_device_argument_checks(tmp_path):
     if _lib.device_count() == 0:
         assert L.sf_index_file_multi(os.fsencode(p), 4096, 1, sig, 4, ctypes.byref(need), bh) == _lib.SF_ENODEV
         assert L.sf_index_device_multi(1, one, 100, 4096, one, 0, 1, None) == _lib.SF_ENODEV
+
+
+def test_table_kernel_is_the_measured_one():
+    """the explicit-list kernel's rate depends on its compiled form
+    (DESIGN.md 3.4); the committed record names the machine code the round-5
+    A/B measured as the shipped form, so a change cannot silently replace it."""
+    import json
+    from syncfast_amd._lib import TABLE_KERNEL, kernel_code_sha256
+    with open(os.path.join(ROOT, "profiles", "r05", "table_kernel.json")) as f:
+        rec = json.load(f)
+    assert rec["symbol"] == TABLE_KERNEL
+    assert kernel_code_sha256(symbol=TABLE_KERNEL) == rec["kernel_code_sha256"], \
+        "the explicit-list kernel changed: re-measure (scripts/gpu_tab_ab.sh) and update the record"
