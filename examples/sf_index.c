@@ -28,10 +28,8 @@
  *     -j N chunker threads, every batch of ~-S MiB of cut files hashed by ONE
  *     sf_index_fds_blocks call while the threads cut the next batch; -q
  *     prints only the first and last file's rows (every file's blocks_hash);
- *     -R: the same pipeline reading every file ONCE, into pinned batch
- *     buffers (sf_host_alloc), cut there in memory and hashed from there by
- *     sf_index_buffer_blocks (DMA in place): the bytes hashed are the bytes
- *     cut, as in the reference's single pass.
+ *     -P n: the whole run n times in one process (the first pays the
+ *     library's stage allocations), a timing line per pass.
  * Regular files (default mode) go through the same one-open form:
  * sf_file_stamp_fd + sf_index_fd_fixed on the open descriptor.
  */
@@ -365,7 +363,6 @@ typedef struct {
     sf_file_stamp st;
     uint64_t *offs, cap, n, bytes;
     uint32_t *sizes;
-    uint64_t slot, slot_len; /* -R: where the file is read in its batch buffer (stat size) */
 } cut_job;
 
 typedef struct {
@@ -375,53 +372,9 @@ typedef struct {
     int *batch_left;         /* files of each batch still being cut */
     int next, hashed;        /* next file to cut; the last batch hashed */
     double chunk_s, open_s, read_s; /* summed over threads: cutting (all of it), its open + stamp, its reads */
-    uint8_t *bufs[2];        /* -R: the pinned batch buffers (batch b in bufs[b & 1]); NULL otherwise */
     pthread_mutex_t mu;
     pthread_cond_t cv;
 } cut_pool;
-
-/* -R: the file read whole into its slot of the batch buffer (one read, as
- * the reference's), then cut there in memory; the descriptor is closed at
- * once.  A file that is not its stat size any more: SF_EAGAIN (indexed again
- * alone). */
-static int cut_in_memory(cut_job *j, uint8_t *dst, double *read_s) {
-    const double t0 = now_s();
-    uint64_t got = 0;
-    while (got < j->slot_len) {
-        const ssize_t r = pread(j->fd, dst + got, j->slot_len - got, (off_t)got);
-        if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) break;
-        got += (uint64_t)r;
-    }
-    uint8_t probe;
-    const int more = got == j->slot_len && pread(j->fd, &probe, 1, (off_t)got) == 1;
-    *read_s += now_s() - t0;
-    close(j->fd);
-    j->fd = -1;
-    if (got != j->slot_len || more) return SF_EAGAIN;
-    j->bytes = got;
-    uint64_t n = 0, start = 0;
-    sf_zpaq z;
-    sf_zpaq_init(&z, 13, 32768); /* ZPAQ_BITS, MAX_BLOCK_SIZE: src/index.rs:40-41 */
-    for (uint64_t p = 0; p < got || start < got;) {
-        const size_t k = p < got ? sf_zpaq_next(&z, dst + p, (size_t)(got - p)) : 0;
-        const uint64_t end = k ? p + k : got;
-        if (n == j->cap) {
-            const uint64_t c2 = j->cap ? 2 * j->cap : 1024;
-            uint64_t *o2 = realloc(j->offs, c2 * sizeof(uint64_t));
-            if (o2) j->offs = o2;
-            uint32_t *s2 = o2 ? realloc(j->sizes, c2 * sizeof(uint32_t)) : NULL;
-            if (s2) j->sizes = s2;
-            if (!o2 || !s2) return SF_ENOMEM;
-            j->cap = c2;
-        }
-        j->offs[n] = start;
-        j->sizes[n++] = (uint32_t)(end - start);
-        start = p = end;
-    }
-    j->n = n;
-    return SF_OK;
-}
 
 static void *cut_worker(void *arg) {
     cut_pool *P = arg;
@@ -440,12 +393,8 @@ static void *cut_worker(void *arg) {
         j->rc = j->fd < 0 ? SF_EIO : !buf ? SF_ENOMEM : sf_file_stamp_fd(j->fd, &j->st);
         const double t1 = now_s();
         double rd = 0;
-        if (P->bufs[0] && j->rc == SF_OK) {
-            j->rc = cut_in_memory(j, P->bufs[P->batch_of[k] & 1] + j->slot, &rd);
-        } else {
-            if (j->rc == SF_OK) j->rc = zpaq_cut_fd(j->fd, buf, kRead, &j->offs, &j->sizes, &j->cap, &j->n, &j->bytes, &rd);
-            if (j->rc == SF_OK && j->bytes != j->st.size) j->rc = SF_EAGAIN;  /* written while cut */
-        }
+        if (j->rc == SF_OK) j->rc = zpaq_cut_fd(j->fd, buf, kRead, &j->offs, &j->sizes, &j->cap, &j->n, &j->bytes, &rd);
+        if (j->rc == SF_OK && j->bytes != j->st.size) j->rc = SF_EAGAIN;  /* written while cut */
         const double dt = now_s() - t0;
         pthread_mutex_lock(&P->mu);
         P->chunk_s += dt;
@@ -459,8 +408,7 @@ static void *cut_worker(void *arg) {
     return NULL;
 }
 
-static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, int timing, int quiet,
-                           int read_once) {
+static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, int timing, int quiet) {
     cut_job *jobs = calloc((size_t)(n ? n : 1), sizeof(cut_job));
     int *batch_of = malloc((size_t)(n ? n : 1) * sizeof(int)), nb = 0;
     int *batch_left = calloc((size_t)(n ? n : 1), sizeof(int)), *batch_first = calloc((size_t)n + 2, sizeof(int));
@@ -478,31 +426,17 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         jobs[k].path = paths[k];
         jobs[k].fd = -1;
         const uint64_t sz = stat(paths[k], &sb) == 0 ? (uint64_t)sb.st_size : 0;
-        const uint64_t slot = (sz + 15) & ~15ull; /* -R: 16-B aligned slots in the batch buffer */
-        if (k == 0 || (read_once ? acc + slot > batch_bytes && acc > 0 : acc >= batch_bytes) ||
-            k - batch_first[nb - 1] >= max_files) {
+        if (k == 0 || acc >= batch_bytes || k - batch_first[nb - 1] >= max_files) {
             batch_first[nb++] = k;
             acc = 0;
         }
         batch_of[k] = nb - 1;
         batch_left[nb - 1]++;
-        jobs[k].slot = acc;
-        jobs[k].slot_len = sz;
-        acc += read_once ? slot : sz;
+        acc += sz;
     }
     batch_first[nb] = n;
-    cut_pool P = {jobs, n, threads, batch_of, batch_left, 0, -1, 0.0, 0.0, 0.0, {NULL, NULL}, PTHREAD_MUTEX_INITIALIZER,
+    cut_pool P = {jobs, n, threads, batch_of, batch_left, 0, -1, 0.0, 0.0, 0.0, PTHREAD_MUTEX_INITIALIZER,
                   PTHREAD_COND_INITIALIZER};
-    uint64_t buf_bytes = 16;
-    if (read_once) { /* two pinned batch buffers, each as large as the largest batch */
-        for (int b = 0; b < nb; b++) {
-            const cut_job *last = &jobs[batch_first[b + 1] - 1];
-            const uint64_t end = last->slot + ((last->slot_len + 15) & ~15ull);
-            if (end > buf_bytes) buf_bytes = end;
-        }
-        for (int i = 0; i < 2; i++)
-            if (sf_host_alloc(buf_bytes, (void **)&P.bufs[i]) != SF_OK) return SF_ENOMEM;
-    }
     pthread_t *th = malloc((size_t)(threads > 0 ? threads : 1) * sizeof(pthread_t));
     int started = 0, rc = th ? SF_OK : SF_ENOMEM;
     for (int t = 0; rc == SF_OK && t < threads; t++)
@@ -536,36 +470,7 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
             cnt[k] = j->rc == SF_OK ? j->n : 0;
         }
         uint32_t bad = 0;
-        if (rc == SF_OK && read_once) {
-            /* one list over the batch buffer (slot + file offset), one call;
-             * rows back to file offsets, each file's blocks_hash from its rows */
-            uint64_t *lo = malloc((rows_n ? rows_n : 1) * sizeof(uint64_t));
-            uint32_t *lz = malloc((rows_n ? rows_n : 1) * sizeof(uint32_t));
-            uint64_t r0 = 0, blen = 0;
-            if (!lo || !lz) rc = SF_ENOMEM;
-            for (int k = 0; rc == SF_OK && k < m; k++) {
-                const cut_job *j = &jobs[f0 + k];
-                first[k] = r0;
-                for (uint64_t i = 0; i < cnt[k]; i++, r0++) {
-                    lo[r0] = j->slot + j->offs[i];
-                    lz[r0] = j->sizes[i];
-                }
-                fst[k] = j->rc;
-                if (j->slot + j->slot_len > blen) blen = j->slot + j->slot_len;
-            }
-            first[m] = r0;
-            if (rc == SF_OK) {
-                const double th0 = now_s();
-                rc = sf_index_buffer_blocks(P.bufs[b & 1], blen, lo, lz, r0, rows, NULL);
-                for (int k = 0; rc == SF_OK && k < m; k++) {
-                    for (uint64_t i = first[k]; i < first[k + 1]; i++) rows[i].offset -= jobs[f0 + k].slot;
-                    rc = sf_blocks_hash_sigs(rows + first[k], first[k + 1] - first[k], hashes + 20 * k);
-                }
-                t_hash += now_s() - th0;
-            }
-            free(lo);
-            free(lz);
-        } else if (rc == SF_OK) {
+        if (rc == SF_OK) {
             const double th0 = now_s();
             const int r = sf_index_fds_blocks(fds, sts, (uint32_t)m, po, pz, cnt, 0, rows, rows_n, first, hashes, fst,
                                               &bad);
@@ -626,7 +531,6 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
                 "\"wait_cut_s\": %.6f}\n",
                 n, threads, nb, (unsigned long long)total_bytes, (unsigned long long)total_blocks, wall, P.chunk_s,
                 P.open_s, P.read_s, t_hash, t_wait);
-    for (int i = 0; i < 2; i++) sf_host_free(P.bufs[i]);
     free(th); free(jobs); free(batch_of); free(batch_left); free(batch_first);
     return rc;
 }
@@ -765,7 +669,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
-    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0, once = 0;
+    int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
     int passes = 1;
     uint64_t batch_mib = 256;
     long long wire = -1, wire_cdc = -1;
@@ -779,7 +683,6 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
         else if (strcmp(argv[i], "-q") == 0) quiet = 1;
-        else if (strcmp(argv[i], "-R") == 0) once = 1;
         else if (i + 1 < argc && strcmp(argv[i], "-P") == 0) passes = atoi(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
         else if (strcmp(argv[i], "-L") == 0) lookup = 1;
@@ -790,7 +693,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-R] [-j threads] [-S batch_mib] [-q] [-P passes]] | -s shards] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-q] [-P passes]] | -s shards] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -826,7 +729,7 @@ int main(int argc, char **argv) {
         int rc = SF_OK;
         for (int pass = 0; pass < passes && rc == SF_OK; pass++)
             rc = index_zpaq_many(argv + i, argc - i, threads > 0 ? threads : 1, batch_mib << 20, timing,
-                                 pass + 1 < passes ? 2 : quiet, once);
+                                 pass + 1 < passes ? 2 : quiet);
         if (rc != SF_OK) fprintf(stderr, "zpaq many: %s\n", sf_strerror(rc));
         sf_release_host_cache();
         return rc != SF_OK;

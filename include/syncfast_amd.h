@@ -234,14 +234,6 @@ int sf_fill_splitmix_device(void *d_out, uint64_t len, uint64_t seed, uint64_t s
 
 /* ------------------------------------------------ host-memory entries */
 
-/* Page-locked host memory owned by the caller (hipHostMalloc): bytes read
- * into it (a caller that reads its files itself, once, for its chunker) go to
- * the device by DMA in place from sf_index_buffer / sf_index_buffer_blocks,
- * with no staging copy and no page locking per call.  sf_host_free(NULL) is
- * SF_OK. */
-int sf_host_alloc(uint64_t bytes, void **out);
-int sf_host_free(void *p);
-
 
 /* End to end from host memory: H2D in pipelined chunks, fixed-tiling kernel,
  * D2H of the signature rows.  Blocking.  out has cap rows. */

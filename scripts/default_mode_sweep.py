@@ -3,8 +3,9 @@ chunker threads x the library's reader threads (SF_IO_THREADS) x batch size,
 on config 3's shape (1024 x 8 MiB) and a 0-200 KiB tree, files in the page
 cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
 
-usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...] [fds,once]
-(once: -R, every file read once into pinned batch buffers and hashed from there)"""
+usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...]
+(round 5 also swept a read-once form, every file read once into pinned
+batch buffers and hashed from there: slower, removed)"""
 import json
 import os
 import shutil
@@ -34,7 +35,7 @@ def main():
     js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "8,12,16").split(",")]
     ios = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8,16").split(",")]
     ss = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "256").split(",")]
-    modes = (sys.argv[4] if len(sys.argv) > 4 else "fds").split(",")
+    modes = ["fds"]
     rng = np.random.default_rng(3)
     small, tot = [], 0
     while tot < (1 << 30):
@@ -49,7 +50,7 @@ def main():
                         env = dict(os.environ, SF_IO_THREADS=str(io))
                         if os.environ.get("TRACE") == "1":
                             env["SF_TRACE"] = "1"
-                        extra = ["-R"] if mode == "once" else []
+                        extra = []
                         r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + extra
                                            + paths,
                                            capture_output=True, text=True, env=env, timeout=300)

@@ -1045,18 +1045,6 @@ static int sf_index_fd_fixed_body(int fd, const sf_file_stamp* expect, uint32_t 
   });
 }
 
-int sf_host_alloc(uint64_t bytes, void** out) {
-  if (!out) return SF_EINVAL;
-  *out = nullptr;
-  if (bytes == 0) return SF_EINVAL;
-  return hip_err(hipHostMalloc(out, bytes, hipHostMallocDefault));
-}
-
-int sf_host_free(void* p) {
-  if (!p) return SF_OK;
-  return hip_err(hipHostFree(p));
-}
-
 int sf_file_stamp_fd(int fd, sf_file_stamp* out) {
   if (fd < 0 || !out) return SF_EINVAL;
   return stamp_of(fd, out, nullptr) ? SF_OK : SF_EIO;

@@ -179,3 +179,33 @@ def test_c_consumer_content_defined_wire_run(gpu, n):
     dig = oracle.index_blocks(data, np.asarray(offs, np.uint64), np.asarray(sizes, np.uint32))
     want = b"".join(wire.write_message("FileBlock", bytes(d), int(s)) for d, s in zip(dig, sizes))
     assert r.stdout == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 4])
+def test_c_consumer_default_mode_many_files(gpu, tmp_path, threads):
+    """examples/sf_index -Z -M: the default mode over many files from C --
+    files cut by the stand-in chunker on `threads` threads over their open
+    descriptors, batches hashed by sf_index_fds_blocks, two passes in one
+    process.  Every row = the stand-in chunker's boundaries (the oracle's
+    copy of it) with the oracle's digests; every blocks_hash = the oracle's."""
+    exe = _built(False)
+    rng = np.random.default_rng(threads)
+    paths, datas = [], []
+    for k, n in enumerate([0, 1, 100_000, 32768, 3 << 20, 777] + [int(x) for x in rng.integers(0, 300_000, 40)]):
+        p = tmp_path / f"f{k:03d}"
+        d = oracle.splitmix_bytes(n, 900 + k)
+        d.tofile(p)
+        paths.append(str(p))
+        datas.append(d)
+    r = subprocess.run([exe, "-Z", "-M", "-P", "2", "-S", "1", "-j", str(threads)] + paths,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = _parse(r.stdout)
+    assert sorted(got) == sorted(paths)
+    for p, d in zip(paths, datas):
+        sizes = oracle.zpaq_standin_sizes(d) if d.size else np.zeros(0, np.uint32)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) if sizes.size else sizes
+        dig = oracle.index_blocks(d, offs, sizes) if sizes.size else np.zeros((0, 20), np.uint8)
+        assert got[p]["rows"] == [(int(o), int(s), bytes(h).hex()) for o, s, h in zip(offs, sizes, dig)], p
+        assert got[p]["bh"] == oracle.blocks_hash(dig).hex(), p
