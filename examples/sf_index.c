@@ -16,6 +16,8 @@
  *     on the host, its blocks hashed by sf_index_buffer_blocks (and again by
  *     sf_index_file_blocks, which must agree);
  *     -s N: each file as N sf_index_file_range shards;
+ *     -X N: each file on N devices of this process (sf_index_file_multi; 0 =
+ *     every visible device);
  *     -w N: N synthetic bytes hashed in HBM, their FILE_BLOCK run to stdout;
  *     -v N: the same bytes cut by the host chunker (-C), hashed as a list in
  *     HBM, the list's FILE_BLOCK run to stdout (sf_wire_blocks_fd);
@@ -146,6 +148,28 @@ static int index_buffer_or_shards(const char *path, uint32_t bs, int shards) {
     if (rc == SF_OK) print_rows(path, rows, n, bh);
     free(rows);
     free(dig);
+    return rc;
+}
+
+/* -X N: one file on N devices from this one process (sf_index_file_multi:
+ * a host thread per device, shard rows at their row offsets, blocks_hash on
+ * the host); the rows and blocks_hash are the one-device route's. */
+static int index_multi(const char *path, uint32_t bs, int ndev) {
+    struct stat sb;
+    if (stat(path, &sb) != 0) return SF_EIO;
+    uint64_t cap = sb.st_size ? ((uint64_t)sb.st_size + bs - 1) / bs : 0, n = 0;
+    uint8_t bh[20];
+    int rc = SF_ENOSPC;
+    sf_block_sig *rows = NULL;
+    for (int attempt = 0; attempt < 3 && rc == SF_ENOSPC; attempt++) { /* the file may grow meanwhile */
+        free(rows);
+        rows = malloc((cap ? cap : 1) * sizeof(sf_block_sig));
+        if (!rows) return SF_ENOMEM;
+        rc = sf_index_file_multi(path, bs, (uint32_t)ndev, rows, cap, &n, bh);
+        if (rc == SF_ENOSPC) cap = n;
+    }
+    if (rc == SF_OK) print_rows(path, rows, n, bh);
+    free(rows);
     return rc;
 }
 
@@ -670,7 +694,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
-    int passes = 1;
+    int passes = 1, multi = -1;
     uint64_t batch_mib = 256;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
@@ -680,6 +704,7 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-w") == 0) wire = atoll(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-v") == 0) wire_cdc = atoll(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-j") == 0) threads = atoi(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-X") == 0) multi = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
         else if (strcmp(argv[i], "-q") == 0) quiet = 1;
@@ -693,7 +718,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-q] [-P passes]] | -s shards] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-q] [-P passes]] | -s shards | -X devices] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -740,7 +765,8 @@ int main(int argc, char **argv) {
         return status;
     }
     for (; i < argc; i++) {
-        const int rc = zpaq  ? index_zpaq(argv[i], timing)
+        const int rc = multi >= 0 ? index_multi(argv[i], bs, multi)
+                       : zpaq  ? index_zpaq(argv[i], timing)
                        : cdc ? index_cdc(argv[i])
                        : (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)
                                                 : index_one(argv[i], bs);
