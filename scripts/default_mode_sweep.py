@@ -35,7 +35,6 @@ def main():
     js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "8,12,16").split(",")]
     ios = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8,16").split(",")]
     ss = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "256").split(",")]
-    modes = ["fds"]
     rng = np.random.default_rng(3)
     small, tot = [], 0
     while tot < (1 << 30):
@@ -45,29 +44,26 @@ def main():
         d = tempfile.mkdtemp(prefix="sf_sw_")
         try:
             paths = write_tree(d, lens, 5)
-            for S, io, j, mode in [(S, io, j, m) for m in modes for S in ss for io in ios for j in js]:
-                    if True:
-                        env = dict(os.environ, SF_IO_THREADS=str(io))
-                        if os.environ.get("TRACE") == "1":
-                            env["SF_TRACE"] = "1"
-                        extra = []
-                        r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + extra
-                                           + paths,
-                                           capture_output=True, text=True, env=env, timeout=300)
-                        if r.returncode:
-                            print(json.dumps({"tree": name, "error": r.stderr[-300:]}), flush=True)
-                            return 1
-                        t = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")][-1]
-                        print(json.dumps({"tree": name, "mode": mode, "j": j, "io": io, "S": S,
-                                          "GB/s": round(t["bytes"] / t["wall_s"] / 1e9, 3),
-                                          "wall": round(t["wall_s"], 3), "hash": round(t["hash_call_s"], 3),
-                                          "wait": round(t["wait_cut_s"], 3), "chunk_cpu": round(t["chunk_cpu_s"], 2),
-                                          "open": round(t["open_s"], 2), "read": round(t["read_s"], 2)}),
-                              flush=True)
-                        if os.environ.get("TRACE") == "1":
-                            tr = [ln for ln in r.stderr.splitlines() if "trace:" in ln]
-                            for ln in tr[:3] + tr[-2:]:
-                                print("   ", ln, flush=True)
+            for S, io, j in [(S, io, j) for S in ss for io in ios for j in js]:
+                env = dict(os.environ, SF_IO_THREADS=str(io))
+                if os.environ.get("TRACE") == "1":
+                    env["SF_TRACE"] = "1"
+                r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + paths,
+                                   capture_output=True, text=True, env=env, timeout=300)
+                if r.returncode:
+                    print(json.dumps({"tree": name, "error": r.stderr[-300:]}), flush=True)
+                    return 1
+                t = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")][-1]
+                print(json.dumps({"tree": name, "j": j, "io": io, "S": S,
+                                  "GB/s": round(t["bytes"] / t["wall_s"] / 1e9, 3),
+                                  "wall": round(t["wall_s"], 3), "hash": round(t["hash_call_s"], 3),
+                                  "wait": round(t["wait_cut_s"], 3), "chunk_cpu": round(t["chunk_cpu_s"], 2),
+                                  "open": round(t["open_s"], 2), "read": round(t["read_s"], 2)}),
+                      flush=True)
+                if os.environ.get("TRACE") == "1":
+                    tr = [ln for ln in r.stderr.splitlines() if "trace:" in ln]
+                    for ln in tr[:3] + tr[-2:]:
+                        print("   ", ln, flush=True)
         finally:
             shutil.rmtree(d, ignore_errors=True)
     return 0

@@ -80,10 +80,12 @@ int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks
   const uint8_t* d = static_cast<const uint8_t*>(d_data);
   uint8_t* o = static_cast<uint8_t*>(d_digests);
   if (weak) {  // opt-in fused Adler-32 (a separate instantiation; the default kernel is unchanged)
+    sfi::clear_stale_error();
     hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1, true>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs,
                        nblocks, o, pad, weak);
     return hip_err(hipGetLastError());
   }
+  sfi::clear_stale_error();
   hipLaunchKernelGGL((sf::sha1_fixed_kernel<kTile, 1>), dim3(grid), dim3(sf::kThreads), 0, stream, d, len, bs, nblocks, o, pad, nullptr);
   return hip_err(hipGetLastError());
 }
@@ -231,6 +233,7 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
       j.waves = (uint32_t)ceil_div(nfiles, 64);
       return launch_chain_helper(j, none, s);
     }
+    sfi::clear_stale_error();
     hipLaunchKernelGGL(sf::sha1_chain_kernel, dim3((unsigned)ceil_div(nfiles, 64)), dim3(64), 0, s, dig, nbf * 20,
                        nfiles, (uint32_t)(nbf * 20), fh);
     return hip_err(hipGetLastError());
@@ -243,6 +246,7 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
   const unsigned chain_wgs = (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
   const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
                      nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, d_status,
                      chain_spin_limit());
@@ -268,6 +272,7 @@ int launch_wire(const uint8_t* d_digests, uint64_t n, uint32_t bs, uint32_t last
     }
     return SF_OK;
   }
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::wire_file_blocks_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, d_digests,
                      n, bs, last, d_out);
   return hip_err(hipGetLastError());
@@ -534,6 +539,7 @@ int sf_fill_splitmix_device(void* d_out, uint64_t len, uint64_t seed, uint64_t s
   if (!d_out) return SF_EINVAL;
   const uint64_t nvec = len / 16 + 1;
   const unsigned grid = (unsigned)std::min<uint64_t>(ceil_div(nvec, 256), 65536);
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::fill_splitmix_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
                      static_cast<uint8_t*>(d_out), len, seed, start);
   return hip_err(hipGetLastError());

@@ -127,6 +127,7 @@ namespace sfi {
 int launch_chain_helper(const sf::ChainJob& j0, const sf::ChainJob& j1, hipStream_t stream) {
   const unsigned grid = j0.waves + j1.waves;
   if (grid == 0) return SF_OK;
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::sha1_chain_helper_kernel, dim3(grid), dim3(sf::kHelperThreads), 0, stream, j0, j1);
   return hip_err(hipGetLastError());
 }

@@ -108,6 +108,14 @@ inline int hip_err(hipError_t e) {
   return SF_ENODEV;
 }
 
+// hipGetLastError() answers the last failing HIP call of this thread, whatever
+// it was, until it is read.  A launcher reads it after its launch, so it first
+// clears what an earlier call left there -- one of ours whose status is
+// ignored on purpose (hipHostUnregister in cleanup, an attribute probe), or
+// the caller's, or another library's on the same thread -- which would
+// otherwise be reported as the launch's failure (SF_ENODEV from a good launch).
+inline void clear_stale_error() { (void)hipGetLastError(); }
+
 inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 inline int check_fixed_args(uint64_t len, uint32_t bs) {

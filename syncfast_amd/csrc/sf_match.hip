@@ -129,6 +129,7 @@ int block_set_build(const void* d_table, const uint8_t* d_present, uint64_t n_ro
   int rc = hip_err(hipMallocAsync(reinterpret_cast<void**>(&bs->slots), cap * sizeof(unsigned long long), s));
   if (rc == SF_OK) rc = hip_err(hipMemsetAsync(bs->slots, 0, cap * sizeof(unsigned long long), s));
   if (rc == SF_OK && n_rows) {
+    sfi::clear_stale_error();
     hipLaunchKernelGGL(sfm::block_set_insert_kernel, dim3((unsigned)ceil_div(n_rows, 256)), dim3(256), 0, s,
                        bs->table, d_present, n_rows, bs->slots, bs->mask);
     rc = hip_err(hipGetLastError());
@@ -161,6 +162,7 @@ int sf_block_set_lookup(const sf_block_set* set, const void* d_query, uint64_t n
   const uint64_t per = 1ull << 31;  // queries per launch (< 2^32 work-items)
   for (uint64_t q0 = 0; q0 < n_query; q0 += per) {
     const uint64_t nq = std::min(per, n_query - q0);
+    sfi::clear_stale_error();
     hipLaunchKernelGGL(sfm::block_set_lookup_kernel, dim3((unsigned)ceil_div(nq, 256)), dim3(256), 0,
                        as_stream(stream), set->table, set->slots, set->mask,
                        static_cast<const uint8_t*>(d_query) + q0 * 20, nq, d_rows + q0);

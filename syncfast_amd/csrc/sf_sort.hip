@@ -179,6 +179,7 @@ template <uint32_t BINS>
 static void class_order_launch(const uint32_t* d_sizes, uint64_t n, uint32_t mbits, uint32_t kmax, uint32_t* hist,
                                uint32_t ntiles, uint32_t* d_order, hipStream_t s) {
   uint32_t* totals = hist + (uint64_t)ntiles * BINS;
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::class_hist_kernel<BINS>, dim3(ntiles), dim3(sf::kSortThreads), 0, s, d_sizes, n, mbits, kmax,
                      hist, ntiles);
   hipLaunchKernelGGL(sf::class_scan_kernel, dim3(BINS), dim3(sf::kSortThreads), 0, s, hist, ntiles, totals);
@@ -211,7 +212,8 @@ extern "C" int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uin
   hipStream_t s = static_cast<hipStream_t>(stream);
   void* ws = nullptr;
   const uint32_t kmax = (16u << (mbits < 4 ? 4 : mbits)) - 1u;
-  if (hipMallocAsync(&ws, sfi::class_order_workspace(n, kmax), s) != hipSuccess) return sfi::hip_err(hipGetLastError());
+  const hipError_t e = hipMallocAsync(&ws, sfi::class_order_workspace(n, kmax), s);
+  if (e != hipSuccess) return sfi::hip_err(e);
   const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, s);
   (void)hipFreeAsync(ws, s);
   return rc;

@@ -67,6 +67,7 @@ int launch_chained(const uint8_t* data, uint64_t len, uint32_t bs, uint64_t nblo
   const uint64_t rest = bwaves > 3 * C ? bwaves - 3 * C : 0;
   const unsigned grid = (unsigned)(C + ceil_div(rest, sf::kWavesPerWG));
   if (grid == 0) return SF_OK;
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::sha1_fixed_chained_kernel<128>, dim3(grid), dim3(sf::kThreads), 0, stream, data, len, bs,
                      nblocks, digests, pad, j0, j1, wpf, wpp, poff);
   return hip_err(hipGetLastError());

@@ -19,6 +19,7 @@ int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, con
   const uint64_t ngroups = (nblocks + 63) / 64;
   const unsigned grid = (unsigned)((ngroups + sf::kTableWG - 1) / sf::kTableWG);
   uint32_t* const next_group = nullptr;
+  sfi::clear_stale_error();
   if (weak_form)
     hipLaunchKernelGGL((sf::sha1_table_kernel<128, true>), dim3(grid), dim3(64 * sf::kTableWG), 0, stream, d_data, len,
                        d_offsets, d_sizes, nblocks, d_digests, d_status, weak, order, next_group);

@@ -89,6 +89,7 @@ int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_
   // is not launched whole
   for (uint64_t first = 0; first < n && rc == SF_OK; first += kWireMaxPerLaunch) {
     const uint64_t cnt = std::min(kWireMaxPerLaunch, n - first);
+    sfi::clear_stale_error();
     hipLaunchKernelGGL(wire_len_kernel, dim3((unsigned)ceil_div(cnt, 256)), dim3(256), 0, s, d_sizes + first, cnt,
                        lens + first);
     rc = hip_err(hipGetLastError());
@@ -109,6 +110,7 @@ int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_
 // d_chunk_ends[k] = end offset of chunk k (chunks of `per` messages).
 int wire_chunk_ends(const uint64_t* d_ends, uint64_t n, uint64_t per, uint64_t* d_chunk_ends, hipStream_t s) {
   const uint64_t nchunks = ceil_div(n, per);
+  sfi::clear_stale_error();
   hipLaunchKernelGGL(wire_chunk_ends_kernel, dim3((unsigned)ceil_div(nchunks, 256)), dim3(256), 0, s, d_ends, n, per,
                      nchunks, d_chunk_ends);
   return hip_err(hipGetLastError());
@@ -120,6 +122,7 @@ int wire_build(const uint8_t* d_digests, const uint32_t* d_sizes, const uint64_t
                uint64_t cnt, uint64_t base, uint8_t* d_out, hipStream_t s) {
   for (uint64_t a = 0; a < cnt; a += kWireMaxPerLaunch) {
     const uint64_t m = std::min(kWireMaxPerLaunch, cnt - a);
+    sfi::clear_stale_error();
     hipLaunchKernelGGL(wire_blocks_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, s,
                        d_digests + (first + a) * 20, d_sizes + first + a, d_ends + first + a, m, base, d_out);
     const int rc = hip_err(hipGetLastError());

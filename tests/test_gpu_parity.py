@@ -296,6 +296,36 @@ def test_small_buffer_and_file_routes(gpu, min_mib, knobs, tmp_path):
         assert np.array_equal(rows["sha1"], want) and bh == oracle.blocks_hash(want)
 
 
+def test_launch_ignores_stale_thread_error(gpu, tmp_path):
+    # a failing HIP call earlier on the same thread (here hipSetDevice on a
+    # device that does not exist, through the runtime the library is linked
+    # against) leaves hipGetLastError() set; the launchers clear it before
+    # their own launch, so it is not reported as a launch failure (round 5's
+    # full GPU run failed once this way: SF_ENODEV from a good in-place call)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    data = oracle.splitmix_bytes((2 << 20) + 13, 99)
+    _, _, want = oracle.index_fixed(data, 4096)
+    offs = np.arange(0, data.size, 5000, dtype=np.uint64)
+    sizes = np.minimum(5000 + (np.arange(offs.size) % 7) * 100, data.size - offs).astype(np.uint32)
+    path = tmp_path / "f.bin"
+    path.write_bytes(data.tobytes())
+    t = to_dev(data.tobytes(), gpu)
+
+    def poison():
+        assert hip.hipSetDevice(ctypes.c_int(1 << 20)) != 0
+    poison()
+    assert np.array_equal(host.index_buffer(data, 4096)["sha1"], want)
+    poison()
+    rows, _ = host.index_buffer_blocks(data, offs, sizes)
+    assert [bytes(r) for r in rows["sha1"][:3]] == [oracle.sha1(data[o:o + s]) for o, s in zip(offs[:3], sizes[:3])]
+    poison()
+    rows, bh = host.index_file(str(path), 4096)
+    assert np.array_equal(rows["sha1"], want) and bh == oracle.blocks_hash(want)
+    poison()
+    assert np.array_equal(device.index_device(t, 4096).cpu().numpy(), want)
+
+
 def test_block_digest_independent_of_neighbours(gpu):
     # the same block bytes at different positions / in different waves give
     # the same digest (no cross-lane leakage through the LDS tile)
