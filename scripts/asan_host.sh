@@ -7,6 +7,9 @@
 # must equal the uninstrumented build's, and ASan must report nothing.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
+for b in ./examples/build/sf_index ./examples/build/asan/sf_index; do
+  [ -x "$b" ] || { echo "missing $b (make -C examples && make -C examples asan, in-tree)"; exit 1; }
+done
 W=$(mktemp -d /tmp/sf_asan.XXXXXX)
 python3 - "$W" <<'EOF'
 import os, sys
@@ -29,6 +32,7 @@ run() {  # name cmd...  (both builds, same input, outputs compared)
   timeout -k 10 300 ./examples/build/asan/sf_index "$@" > "$W/$name.asan" 2> "gpurun_out/asan_$name.err" < "$W/f07"
   local r=$?
   if [ $r -ne 0 ]; then echo "$name: asan build rc=$r"; tail -30 "gpurun_out/asan_$name.err"; return 1; fi
+  [ -s "$W/$name.asan" ] || { echo "$name: no output"; return 1; }
   cmp -s "$W/$name.plain" "$W/$name.asan" || { echo "$name: outputs differ"; return 1; }
   echo "$name: ok ($(wc -l < "$W/$name.asan") lines, asan clean)"
 }
@@ -52,18 +56,21 @@ run zpaq_many_small -Z -M -j 4 -S 1 "$W"/s* || rc=1
 run multi -X 0 -b 4096 "$W"/f0* || rc=1  # one file on every visible device from one process
 run wire_cdc -v 20000001 || rc=1
 # every route over the same files gives the same rows and blocks_hash
-cmp -s "$W/zpaq.asan" "$W/zpaq_many.asan" && echo "zpaq_many == zpaq: ok" || { echo "zpaq_many differs from zpaq"; rc=1; }
+same() { [ -s "$1" ] && cmp -s "$1" "$2"; }  # equal, and not two empty outputs
+same "$W/zpaq.asan" "$W/zpaq_many.asan" && echo "zpaq_many == zpaq: ok" || { echo "zpaq_many differs from zpaq"; rc=1; }
 for m in buffer shards inplace inplace_bounce multi; do
-  cmp -s "$W/files.asan" "$W/$m.asan" && echo "$m == files: ok" || { echo "$m differs from files"; rc=1; }
+  same "$W/files.asan" "$W/$m.asan" && echo "$m == files: ok" || { echo "$m differs from files"; rc=1; }
 done
 mkfifo "$W/pipe"
-( sleep 1; cat "$W/f08" > "$W/pipe" ) &
+# the writer's open of the FIFO is inside its own time limit: if the reader
+# never opens the other end, the writer still ends and `wait` returns
+( sleep 1; timeout -k 5 100 sh -c 'cat "$1" > "$2"' sh "$W/f08" "$W/pipe" ) &
 timeout -k 10 120 ./examples/build/asan/sf_index -b 4096 "$W/pipe" > "$W/fifo.asan" 2> gpurun_out/asan_fifo.err
 r=$?; wait
 if [ $r -ne 0 ]; then echo "fifo: asan build rc=$r"; tail -30 gpurun_out/asan_fifo.err; rc=1
 else
   ./examples/build/sf_index -b 4096 "$W/f08" | sed "s|$W/f08|$W/pipe|" > "$W/fifo.plain"
-  cmp -s "$W/fifo.plain" "$W/fifo.asan" && echo "fifo: ok (asan clean)" || { echo "fifo: outputs differ"; rc=1; }
+  same "$W/fifo.plain" "$W/fifo.asan" && echo "fifo: ok (asan clean)" || { echo "fifo: outputs differ"; rc=1; }
 fi
 rm -rf "$W"
 exit $rc

@@ -41,9 +41,9 @@ if [ -n "$CDC" ]; then
   run cdc_prof 900 bash scripts/cdc_prof.sh gpurun_out/cdc || exit $?
 fi
 if [ -n "$PROFILE" ]; then
-  # --no-e2e --no-cdc-list: only the timed kernel launches, so rocprof's average is the
+  # --no-e2e --no-cdc-list --no-default-mode: only the timed kernel launches, so rocprof's average is the
   # bench line's kernel_ms (the end-to-end leg launches 256 MiB stages)
-  B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-cdc-list"
+  B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-cdc-list --no-default-mode"
   run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B || exit $?
   run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o pmc -- $B || exit $?
   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o pmc -- $B || exit $?
