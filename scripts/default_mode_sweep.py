@@ -3,7 +3,9 @@ chunker threads x the library's reader threads (SF_IO_THREADS) x batch size,
 on config 3's shape (1024 x 8 MiB) and a 0-200 KiB tree, files in the page
 cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
 
-usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...]
+usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...] [reps]
+FORMS=ramp,flat: the batch plan (ramp = batch_target, the default; flat = -F,
+every batch S MiB), interleaved within each setting.
 (round 5 also swept a read-once form, every file read once into pinned
 batch buffers and hashed from there: slower, removed)"""
 import json
@@ -35,6 +37,8 @@ def main():
     js = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "8,12,16").split(",")]
     ios = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8,16").split(",")]
     ss = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "256").split(",")]
+    reps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    forms = os.environ.get("FORMS", "ramp").split(",")
     rng = np.random.default_rng(3)
     small, tot = [], 0
     while tot < (1 << 30):
@@ -44,17 +48,20 @@ def main():
         d = tempfile.mkdtemp(prefix="sf_sw_")
         try:
             paths = write_tree(d, lens, 5)
-            for S, io, j in [(S, io, j) for S in ss for io in ios for j in js]:
+            for S, io, j, form, rep in [(S, io, j, f, r) for S in ss for io in ios for j in js
+                                        for r in range(reps) for f in forms]:
                 env = dict(os.environ, SF_IO_THREADS=str(io))
                 if os.environ.get("TRACE") == "1":
                     env["SF_TRACE"] = "1"
-                r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + paths,
+                flags = ["-F"] if form == "flat" else []
+                r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + flags + paths,
                                    capture_output=True, text=True, env=env, timeout=300)
                 if r.returncode:
                     print(json.dumps({"tree": name, "error": r.stderr[-300:]}), flush=True)
                     return 1
                 t = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")][-1]
-                print(json.dumps({"tree": name, "j": j, "io": io, "S": S,
+                print(json.dumps({"tree": name, "form": form, "rep": rep, "j": j, "io": io, "S": S,
+                                  "batches": t["batches"],
                                   "GB/s": round(t["bytes"] / t["wall_s"] / 1e9, 3),
                                   "wall": round(t["wall_s"], 3), "hash": round(t["hash_call_s"], 3),
                                   "wait": round(t["wait_cut_s"], 3), "chunk_cpu": round(t["chunk_cpu_s"], 2),
