@@ -5,7 +5,8 @@ cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
 
 usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...] [reps]
 FORMS=ramp,flat: the batch plan (ramp = batch_target, the default; flat = -F,
-every batch S MiB), interleaved within each setting.
+every batch S MiB), interleaved within each setting; FORM@DIR runs the
+consumer against DIR/libsyncfast_amd.so (LD_LIBRARY_PATH before its RUNPATH).
 (round 5 also swept a read-once form, every file read once into pinned
 batch buffers and hashed from there: slower, removed)"""
 import json
@@ -51,9 +52,11 @@ def main():
             for S, io, j, form, rep in [(S, io, j, f, r) for S in ss for io in ios for j in js
                                         for r in range(reps) for f in forms]:
                 env = dict(os.environ, SF_IO_THREADS=str(io))
+                if "@" in form:
+                    env["LD_LIBRARY_PATH"] = os.path.abspath(form.split("@", 1)[1])
                 if os.environ.get("TRACE") == "1":
                     env["SF_TRACE"] = "1"
-                flags = ["-F"] if form == "flat" else []
+                flags = ["-F"] if form.split("@")[0] == "flat" else []
                 r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + flags + paths,
                                    capture_output=True, text=True, env=env, timeout=300)
                 if r.returncode:

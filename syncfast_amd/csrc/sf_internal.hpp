@@ -5,7 +5,10 @@
 //   sf_host.cpp   the host-memory entry points: per-device cache of streams
 //                 and staging buffers, the buffer / file / fd / range
 //                 pipelines, the wire stream, host SHA-1 helpers;
-//   sf_files.cpp  sf_index_files, the many-file pipeline.
+//   sf_files.cpp  sf_index_files, the many-file pipeline;
+//   sf_fds.cpp    sf_index_fds_blocks, the default mode over many files;
+//   sf_multi.cpp  one process, N devices;
+//   sf_pool.cpp   the host worker threads of every pipeline (run_pool).
 // The .cpp files use only the HIP runtime API (no kernels), so they build
 // with the host compiler.
 #pragma once
@@ -19,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <system_error>
@@ -84,20 +88,19 @@ inline int guarded(F&& body) noexcept {
   }
 }
 
-// Runs `worker` on the calling thread and on up to nthreads-1 more.  The
-// workers share an atomic work counter, so a thread the system refuses only
-// lowers the parallelism; every started thread is joined before returning
-// (a joinable std::thread destroyed during unwinding would terminate).
+// Runs `worker` on the calling thread and on up to nthreads-1 of the
+// library's kept helper threads (sf_pool.cpp).  The workers share an atomic
+// work counter, so helpers busy elsewhere or a thread the system refuses only
+// lower the parallelism.  Returns when every helper that started the worker
+// has finished it; an exception from any of them is rethrown here.
+void run_pool_fn(unsigned nthreads, const std::function<void()>& worker);
 template <typename F>
 inline void run_pool(unsigned nthreads, F&& worker) {
-  std::vector<std::thread> pool;
-  try {
-    pool.reserve(nthreads);
-    for (unsigned t = 1; t < nthreads; t++) pool.emplace_back(worker);
-  } catch (...) {
+  if (nthreads <= 1) {
+    worker();
+    return;
   }
-  worker();
-  for (auto& th : pool) th.join();
+  run_pool_fn(nthreads, std::function<void()>(std::ref(worker)));
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

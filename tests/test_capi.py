@@ -5,6 +5,7 @@ import ctypes
 import hashlib
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -586,3 +587,29 @@ def test_table_kernel_is_the_measured_one():
     assert rec["symbol"] == TABLE_KERNEL
     assert kernel_code_sha256(symbol=TABLE_KERNEL) == rec["kernel_code_sha256"], \
         "the explicit-list kernel changed: re-measure (scripts/gpu_tab_ab.sh) and update the record"
+
+
+def _cxx_sanitizer_works(flag, tmp_path):
+    src = tmp_path / "probe.cpp"
+    src.write_text("#include <thread>\nint main(){std::thread t([]{});t.join();}\n")
+    r = subprocess.run(["g++", "-std=c++17", "-pthread", flag, str(src), "-o", str(tmp_path / "probe")],
+                       capture_output=True)
+    return r.returncode == 0 and subprocess.run([str(tmp_path / "probe")], capture_output=True).returncode == 0
+
+
+@pytest.mark.parametrize("sanitizer", ["-fsanitize=thread", "-fsanitize=address,undefined"])
+def test_host_pool_stress(tmp_path, sanitizer):
+    """The kept host worker threads every pipeline stage uses (sf_pool.cpp):
+    concurrent callers, nested pools, a worker that throws; every work item
+    runs exactly once, under ThreadSanitizer and under ASan + UBSan (the pool
+    is host code: built here with g++ from the library's own source)."""
+    if not _cxx_sanitizer_works(sanitizer, tmp_path):
+        pytest.skip(f"g++ {sanitizer} unavailable")
+    root = os.path.join(os.path.dirname(__file__), "..")
+    exe = tmp_path / "pool_stress"
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", sanitizer, "-I/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", os.path.join(root, "tests", "native", "pool_stress.cpp"),
+                    os.path.join(root, "syncfast_amd", "csrc", "sf_pool.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and "pool_stress ok" in r.stdout, r.stderr[-2000:]
