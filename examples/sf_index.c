@@ -374,8 +374,7 @@ static int zpaq_cut_fd(int fd, uint8_t *buf, size_t bufsz, uint64_t **offs_io, u
 }
 
 /* -Z -M: index_path's default mode from C.  Files are stat'ed and dealt into
- * batches of about batch_bytes (smaller at both ends: batch_target); `threads`
- * chunker threads take the files in
+ * batches of about batch_bytes; `threads` chunker threads take the files in
  * order (opening each once, stamping it, cutting it over the open descriptor)
  * but never more than one batch ahead of the hashing; the main thread hashes
  * each batch with ONE sf_index_fds_blocks on those descriptors as soon as all
@@ -433,19 +432,6 @@ static void *cut_worker(void *arg) {
     return NULL;
 }
 
-/* Batch b's target size.  The pipeline's fill (the first batch is cut before
- * any hashing starts) and its drain (the last batches are hashed after the
- * last cut) each cost about one batch, so the first batches ramp up from
- * batch/16 and the last ones take half of what is left, down to batch/16.
- * flat (-F): every batch `batch` bytes (the first form). */
-static uint64_t batch_target(uint64_t batch, int b, uint64_t left, int flat) {
-    if (flat) return batch;
-    const uint64_t lo = batch / 16 ? batch / 16 : 1;
-    uint64_t t = b < 4 ? lo << b : batch;
-    if (t > left / 2) t = left / 2;
-    return t < lo ? lo : t > batch ? batch : t;
-}
-
 typedef struct {
     char **paths;
     uint64_t *sizes;
@@ -462,7 +448,8 @@ static void *stat_worker(void *arg) { /* the sizes for the batch plan, 64 files 
     return NULL;
 }
 
-static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, int flat, int timing, int quiet) {
+static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, uint64_t stage_bytes, int timing,
+                           int quiet) {
     cut_job *jobs = calloc((size_t)(n ? n : 1), sizeof(cut_job));
     int *batch_of = malloc((size_t)(n ? n : 1) * sizeof(int)), nb = 0;
     int *batch_left = calloc((size_t)(n ? n : 1), sizeof(int)), *batch_first = calloc((size_t)n + 2, sizeof(int));
@@ -477,7 +464,7 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         max_files = rl.rlim_cur / 4 > 16 ? (int)(rl.rlim_cur / 4) : 16;
     /* the files' sizes, stat'ed on the chunker threads (a stat can cost
      * ~100 us on some hosts: 10,000 files would be a second on one thread) */
-    uint64_t *fsize = calloc((size_t)(n ? n : 1), sizeof(uint64_t)), left = 0, target = 0;
+    uint64_t *fsize = calloc((size_t)(n ? n : 1), sizeof(uint64_t));
     if (!fsize) return SF_ENOMEM;
     {
         stat_pool S = {paths, fsize, n, 0};
@@ -488,19 +475,16 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         stat_worker(&S);
         for (int t = 0; t < ns; t++) pthread_join(st[t], NULL);
     }
-    for (int k = 0; k < n; k++) left += fsize[k];
     for (int k = 0; k < n; k++) { /* batches by size and descriptor count */
         jobs[k].path = paths[k];
         jobs[k].fd = -1;
-        if (k == 0 || acc >= target || k - batch_first[nb - 1] >= max_files) {
+        if (k == 0 || acc >= batch_bytes || k - batch_first[nb - 1] >= max_files) {
             batch_first[nb++] = k;
             acc = 0;
-            target = batch_target(batch_bytes, nb - 1, left, flat);
         }
         batch_of[k] = nb - 1;
         batch_left[nb - 1]++;
         acc += fsize[k];
-        left -= fsize[k];
     }
     batch_first[nb] = n;
     free(fsize);
@@ -541,8 +525,8 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         uint32_t bad = 0;
         if (rc == SF_OK) {
             const double th0 = now_s();
-            const int r = sf_index_fds_blocks(fds, sts, (uint32_t)m, po, pz, cnt, 0, rows, rows_n, first, hashes, fst,
-                                              &bad);
+            const int r = sf_index_fds_blocks(fds, sts, (uint32_t)m, po, pz, cnt, stage_bytes, rows, rows_n, first,
+                                              hashes, fst, &bad);
             t_hash += now_s() - th0;
             if (r != SF_OK && !(r == fst[bad])) rc = r; /* a per-file failure is handled per file */
         }
@@ -739,8 +723,8 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
-    int passes = 1, multi = -1, flat = 0;
-    uint64_t batch_mib = 256;
+    int passes = 1, multi = -1;
+    uint64_t batch_mib = 256, stage_mib = 0;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -751,8 +735,8 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-j") == 0) threads = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-X") == 0) multi = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
+        else if (i + 1 < argc && strcmp(argv[i], "-G") == 0) stage_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
-        else if (strcmp(argv[i], "-F") == 0) flat = 1;
         else if (strcmp(argv[i], "-q") == 0) quiet = 1;
         else if (i + 1 < argc && strcmp(argv[i], "-P") == 0) passes = atoi(argv[++i]);
         else if (strcmp(argv[i], "-m") == 0) many = 1;
@@ -764,7 +748,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-F] [-q] [-P passes]] | -s shards | -X devices] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -799,7 +783,7 @@ int main(int argc, char **argv) {
          * pays the library's stage allocations and first launches) */
         int rc = SF_OK;
         for (int pass = 0; pass < passes && rc == SF_OK; pass++)
-            rc = index_zpaq_many(argv + i, argc - i, threads > 0 ? threads : 1, batch_mib << 20, flat, timing,
+            rc = index_zpaq_many(argv + i, argc - i, threads > 0 ? threads : 1, batch_mib << 20, stage_mib << 20, timing,
                                  pass + 1 < passes ? 2 : quiet);
         if (rc != SF_OK) fprintf(stderr, "zpaq many: %s\n", sf_strerror(rc));
         sf_release_host_cache();

@@ -4,9 +4,11 @@ on config 3's shape (1024 x 8 MiB) and a 0-200 KiB tree, files in the page
 cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
 
 usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...] [reps]
-FORMS=ramp,flat: the batch plan (ramp = batch_target, the default; flat = -F,
-every batch S MiB), interleaved within each setting; FORM@DIR runs the
-consumer against DIR/libsyncfast_amd.so (LD_LIBRARY_PATH before its RUNPATH).
+FORMS=base,base+G64,...: forms interleaved within each setting; +G64 passes
+-G 64 (stages of 64 MiB inside each sf_index_fds_blocks call); FORM@DIR runs
+the consumer against DIR/libsyncfast_amd.so (LD_LIBRARY_PATH before its
+RUNPATH).  (Round 5 also measured a batch plan that ramped the first and
+last batches down, with no gain: removed)
 (round 5 also swept a read-once form, every file read once into pinned
 batch buffers and hashed from there: slower, removed)"""
 import json
@@ -39,7 +41,7 @@ def main():
     ios = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8,16").split(",")]
     ss = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "256").split(",")]
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    forms = os.environ.get("FORMS", "ramp").split(",")
+    forms = os.environ.get("FORMS", "base").split(",")
     rng = np.random.default_rng(3)
     small, tot = [], 0
     while tot < (1 << 30):
@@ -56,7 +58,8 @@ def main():
                     env["LD_LIBRARY_PATH"] = os.path.abspath(form.split("@", 1)[1])
                 if os.environ.get("TRACE") == "1":
                     env["SF_TRACE"] = "1"
-                flags = ["-F"] if form.split("@")[0] == "flat" else []
+                plan = form.split("@")[0].split("+")  # "base+G64": 64 MiB stages per call
+                flags = [a for g in plan[1:] for a in ("-G", g[1:])]
                 r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + flags + paths,
                                    capture_output=True, text=True, env=env, timeout=300)
                 if r.returncode:

@@ -221,10 +221,20 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
   for (size_t k = 0; k < stages.size(); k++)
     for (uint32_t f : stages[k].files)
       if ((first_row[f + 1] - first_row[f]) * 20 > kDevChainMaxRun) dev_bh[k] = 0;
-  auto harvest = [&](size_t k) {  // SF_OK, or the stage's device status (SF_ETIMEDOUT)
+  // A stage whose device blocks_hash lanes gave up waiting (SF_ETIMEDOUT, a
+  // backstop never expected: sha1_staged_kernel) still has every digest --
+  // the launch finished before the D2H -- so its blocks_hash values are
+  // computed on the host instead (counted: "chain_recovered").  Seen once in
+  // round 5 (profiles/r05/pool/ab_2.log), never reproduced.
+  auto harvest = [&](size_t k) {  // SF_OK, or an unknown device status
     const FileStage& st = stages[k];
     const int b = (int)(k & 1);
-    if (dev_bh[k] && stat_host(b) != SF_OK) return stat_host(b);
+    bool host_bh = !dev_bh[k];
+    if (dev_bh[k] && stat_host(b) != SF_OK) {
+      if (stat_host(b) != SF_ETIMEDOUT) return stat_host(b);
+      host_bh = true;
+      stat_add(S_CHAIN_RECOVERED);
+    }
     const uint8_t* dg = static_cast<const uint8_t*>(pdig[b].p);
     const uint8_t* fh = static_cast<const uint8_t*>(pfh[b].p);
     uint64_t r = 0;
@@ -237,7 +247,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
         o[i].size = (uint32_t)std::min<uint64_t>(bs, size[f] - i * bs);
         memcpy(o[i].sha1, dg + 20 * r, 20);
       }
-      if (dev_bh[k]) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
+      if (!host_bh) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
       else sf_host_sha1_impl(dg + 20 * (r - nb), nb * 20, blocks_hashes + 20ull * f, 0);
     }
     return SF_OK;

@@ -191,17 +191,6 @@ def _sizes_ok(sizes, n: int) -> List[int]:
     return sizes
 
 
-
-def _batch_target(batch: int, b: int, left: int) -> int:
-    """Bytes of files for batch b of the default mode's many-file pipeline,
-    `left` bytes of files from its first one on: the first batches ramp up
-    from batch/16 (the first batch is cut before any hashing starts) and the
-    last ones take half of what is left, down to batch/16 (the last batches
-    are hashed after the last cut); batch_target in examples/sf_index.c."""
-    lo = max(1, batch // 16)
-    t = lo << b if b < 4 else batch
-    return max(lo, min(batch, t, left // 2))
-
 def _offsets(sizes) -> np.ndarray:
     offs = np.zeros(len(sizes), np.uint64)
     if len(sizes) > 1:
@@ -582,8 +571,7 @@ class Index:
         file."""
         self._need_chunker()
         todo: List[Tuple[Path, PurePath]] = []
-        sizes: List[int] = []  # each file's size at the walk (a hint for the batch plan)
-        self._index_path_rec(Path(path), PurePath(""), todo, sizes)
+        self._index_path_rec(Path(path), PurePath(""), todo)
         if not todo:
             return
         if batch_bytes <= 0:
@@ -592,24 +580,20 @@ class Index:
             return
         if isinstance(self.chunker, BoundaryChunker):
             if self.chunker.stream:
-                self._index_batched_fds(todo, batch_bytes, chunk_threads, sizes)
+                self._index_batched_fds(todo, batch_bytes, chunk_threads)
             else:
                 self._index_batched_boundaries(todo, batch_bytes)
             return
         self._index_batched(todo, batch_bytes)
 
-    def _index_path_rec(self, root: Path, rel: PurePath, todo, sizes=None) -> None:
+    def _index_path_rec(self, root: Path, rel: PurePath, todo) -> None:
         p = root / rel
-        try:
-            st = os.stat(p)  # is_dir()'s stat, its size kept
-        except OSError:
-            st = None  # as is_dir(): not a directory; the open reports it
-        if st is not None and stat.S_ISDIR(st.st_mode):
+        if p.is_dir():
             log.info("Indexing directory %s (%s)", rel, p)
             for entry in os.listdir(p):  # readdir order, as read_dir (src/index.rs:698)
                 if entry == INDEX_FILE_NAME:
                     continue
-                self._index_path_rec(root, rel / entry, todo, sizes)
+                self._index_path_rec(root, rel / entry, todo)
         else:
             if rel.parts[:1] == (".",):
                 rel = PurePath(*rel.parts[1:])
@@ -618,8 +602,6 @@ class Index:
             name = "" if rel == PurePath("") else rel
             log.info("Indexing file %s (%s)", rel, p)
             todo.append((p, name))
-            if sizes is not None:
-                sizes.append(st.st_size if st is not None and stat.S_ISREG(st.st_mode) else 0)
 
     def _index_batched(self, todo, batch_bytes: int) -> None:
         """Every file needing (re)indexing through ONE native pipeline
@@ -648,7 +630,7 @@ class Index:
             self._insert_rows(file_id, rows, int(first[k]), int(first[k + 1]))
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
 
-    def _index_batched_fds(self, todo, batch_bytes: int, chunk_threads: int, sizes=None) -> None:
+    def _index_batched_fds(self, todo, batch_bytes: int, chunk_threads: int) -> None:
         """The default (content-defined) mode over many files, the files cut
         in parallel and hashed as ONE pipeline per batch.
 
@@ -657,9 +639,7 @@ class Index:
         reference's); the chunker streams the open file on a pool thread; a
         batch of about `batch_bytes` of cut files (and at most a quarter of
         the descriptor limit) goes to sf_index_fds_blocks on those same
-        descriptors while the pool cuts the next batch; the first batches
-        ramp up and the last ones shrink (_batch_target, from the walk's
-        sizes), so the pipeline's fill and drain are small.  A file written while
+        descriptors while the pool cuts the next batch.  A file written while
         it was cut or read (SF_EAGAIN for it alone) is indexed again through
         index_file, in its place, so rows stay in walk order; a FIFO in the
         tree is indexed through index_file from its own open."""
@@ -705,12 +685,9 @@ class Index:
 
         prev = None
         batch, futs, nbytes = [], [], 0
-        hints = list(sizes) if sizes is not None and len(sizes) == len(todo) else [batch_bytes] * len(todo)
-        left, nbatch, target = sum(hints), 0, batch_bytes
         pool = ThreadPoolExecutor(max_workers=threads)
         try:
-            for (p, rel), hint in zip(todo, hints):
-                left -= hint
+            for p, rel in todo:
                 f = open(p, "rb")  # File::open first: same error on a missing file
                 try:
                     if not _seekable(f):  # a FIFO: read from its own open, sequentially
@@ -726,13 +703,10 @@ class Index:
                 if up_to_date:
                     f.close()
                     continue
-                if not batch:  # this file opens batch nbatch
-                    target = _batch_target(batch_bytes, nbatch, left + hint)
-                    nbatch += 1
                 batch.append((file_id, p, rel, f, stamp))
                 futs.append(pool.submit(cut, f, stamp))
                 nbytes += stamp.size
-                if nbytes >= target or len(batch) >= max_files:
+                if nbytes >= batch_bytes or len(batch) >= max_files:
                     if prev is not None:
                         finish(*prev)  # hashed while the pool cuts this batch
                     prev, batch, futs, nbytes = (batch, futs), [], [], 0

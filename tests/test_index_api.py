@@ -540,42 +540,6 @@ def test_index_path_stream_chunker_many_files(tmp_path, monkeypatch, threads, ba
     assert idx.db.execute("SELECT COUNT(*) FROM blocks").fetchone()[0] == before
 
 
-def test_batch_target_ramps_at_both_ends():
-    """The many-file default mode's batch plan (index._batch_target, the same
-    rule as batch_target in examples/sf_index.c): batch/16 doubling up to the
-    batch at the start, half of what is left at the end, never below batch/16
-    nor above the batch."""
-    from syncfast_amd.index import _batch_target
-    B = 256
-    assert [_batch_target(B, b, 1 << 40) for b in range(6)] == [16, 32, 64, 128, 256, 256]
-    assert [_batch_target(B, 9, left) for left in (1 << 40, 512, 300, 100, 20, 0)] == [256, 256, 150, 50, 16, 16]
-    assert _batch_target(5, 0, 1 << 40) == 1 and _batch_target(5, 7, 1 << 40) == 5
-
-
-def test_index_path_stream_chunker_batches_ramp(tmp_path, monkeypatch):
-    """index_path's default mode hands sf_index_fds_blocks small batches first
-    and last (the pipeline's fill and drain), full ones in between."""
-    from syncfast_amd import host
-    _oracle_device_calls(monkeypatch)
-    inner = host.index_fds_blocks
-    calls = []
-
-    def counting(fds, lists, stamps=None, stage_bytes=0):
-        calls.append(sum(os.fstat(fd).st_size for fd in fds))
-        return inner(fds, lists, stamps, stage_bytes)
-
-    monkeypatch.setattr(host, "index_fds_blocks", counting)
-    root = tmp_path / "tree"
-    root.mkdir()
-    for k in range(200):
-        (root / f"f{k:03d}").write_bytes(oracle.splitmix_bytes(1000, 4600 + k).tobytes())
-    idx = Index.open_in_memory(chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
-    idx.index_path(root, batch_bytes=16_000, chunk_threads=2)
-    assert sum(calls) == 200_000
-    assert calls[:4] == [1000, 2000, 4000, 8000] and max(calls) == 16_000
-    assert calls[-1] <= 2000 and calls[-2] <= 4000
-
-
 def test_index_path_stream_chunker_file_changed_is_reindexed(tmp_path, monkeypatch):
     """A file the many-file call reports SF_EAGAIN for (written while it was
     read) is indexed again in its place; its rows are the new bytes'."""
