@@ -12,7 +12,11 @@
 // (others busy, or the system refused a thread) only loses parallelism; a
 // helper that starts after the work is taken finds none and returns.
 // Helpers are never stopped: the pool lives until the process exits (it is
-// never destroyed from a static destructor, like the device resources).
+// never destroyed from a static destructor, like the device resources); a
+// fork()ed child starts a fresh one.
+#include <pthread.h>
+
+#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -65,9 +69,20 @@ struct Pool {
   }
 };
 
+// The pool: never freed, its helpers wait in it until exit.  A child made by
+// fork() has none of the parent's helpers, and may have copied the mutex
+// locked: it starts from a fresh pool (the old one is left as it is).
+std::atomic<Pool*> g_pool{nullptr};
+std::once_flag g_pool_once;
+
+void fresh_pool_in_child() { g_pool.store(new Pool, std::memory_order_release); }
+
 Pool* pool() {
-  static Pool* p = new Pool;  // never freed: its helpers wait in it until exit
-  return p;
+  std::call_once(g_pool_once, [] {
+    g_pool.store(new Pool, std::memory_order_release);
+    pthread_atfork(nullptr, nullptr, fresh_pool_in_child);
+  });
+  return g_pool.load(std::memory_order_acquire);
 }
 
 }  // namespace

@@ -3,6 +3,9 @@
 // tests/test_capi.py::test_host_pool_stress: concurrent callers, nested
 // calls from a helper, workers that throw, and callers that finish their
 // work before any helper starts.  Every work item must run exactly once.
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cstdio>
 #include <stdexcept>
@@ -73,6 +76,29 @@ int main() {
     }
     if (!caught) return fail("exception not rethrown");
   }
+  // a fork()ed child (no helpers of its own; the parent's mutex may have been
+  // copied locked) runs its pools on a fresh pool (not under ThreadSanitizer,
+  // which does not support threads started after a multi-threaded fork)
+#ifndef __SANITIZE_THREAD__
+  {
+    std::atomic<bool> stop{false};
+    std::thread busy([&] {  // keeps the parent's pool mutex busy while we fork
+      while (!stop.load()) sweep(16, 64, false);
+    });
+    for (int r = 0; r < 20; r++) {
+      const pid_t pid = fork();
+      if (pid == 0) _exit(sweep(16, 1000, true) ? 0 : 3);
+      int st = 0;
+      if (pid < 0 || waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+        stop = true;
+        busy.join();
+        return fail("fork child");
+      }
+    }
+    stop = true;
+    busy.join();
+  }
+#endif
   std::printf("pool_stress ok\n");
   return 0;
 }
