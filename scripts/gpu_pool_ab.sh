@@ -3,6 +3,10 @@
 # kept helper threads vs threads started per stage (build_ab/old = the
 # library before the pool, built from an earlier commit), on the consumer's
 # many-file route and on the library's file routes (scripts/pool_ab.py).
+# build_ab/old (git-ignored, removed after the round-5 A/B):
+#   git archive 239da2a syncfast_amd/csrc include | tar -x -C /tmp/o && \
+#   mkdir -p /tmp/o/syncfast_amd/lib && make -C /tmp/o/syncfast_amd/csrc && \
+#   mkdir -p build_ab/old && cp /tmp/o/syncfast_amd/lib/libsyncfast_amd.so build_ab/old/
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 set -o pipefail
 OUT=gpurun_out/${POOL_OUT:-pool}
