@@ -105,6 +105,24 @@ def test_many_small_files_and_reference_kat(gpu, tmp_path):
     assert bytes(hashes[300]).hex() == "84c25d78edcdb67631639c43604cf0149564f044"
 
 
+def test_more_blocks_than_a_stage_holds(gpu, tmp_path):
+    """A file of 4.5 M tiny blocks (1-3 B): more blocks than one stage takes
+    (2^22), so its window splits by block count, not bytes, and its
+    blocks_hash is streamed over the pieces; the files around it stay exact."""
+    rng = np.random.default_rng(7150)
+    tiny = rng.integers(1, 4, 4_500_000).astype(np.uint32)
+    n = int(tiny.sum())
+    p = tmp_path / "tiny"
+    data = oracle.splitmix_bytes(n, 7151).tobytes()
+    p.write_bytes(data)
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    files = (_tree(tmp_path / "a", [1 * MIB + 3], 7152) + [(p, data, _offs(tiny), tiny)]
+             + _tree(tmp_path / "b", [200 * KIB, 0, 9], 7160))
+    rows, first, hashes, status = _run(files)
+    _check(files, rows, first, hashes, status)
+
+
 def test_odd_lists(gpu, tmp_path):
     """Lists a chunker would not make but the contract allows: gaps, overlaps,
     empty blocks, blocks not covering the file, a 4 KiB fixed-like list."""
