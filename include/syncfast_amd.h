@@ -359,10 +359,9 @@ void sf_free_rows(sf_block_sig *rows);
  * blocks_hashes: 20 B per file.  *n_out = total rows (the need, with
  * SF_ENOSPC, checked before any file is read).  On SF_EIO (open, stat or a
  * short read: the file changed while being indexed) *bad_file (may be NULL)
- * is the index of the failing file.  A stage whose device blocks_hash lanes
- * gave up waiting (the fused launch's backstop, see sf_index_device_batch)
- * has its blocks_hash values computed on the host from its digests instead:
- * the call never returns SF_ETIMEDOUT.  Blocking. */
+ * is the index of the failing file.  Each stage's blocks take the batch path
+ * that never waits (sf_index_device_batch with no status word): the call
+ * never returns SF_ETIMEDOUT.  Blocking. */
 int sf_index_files(const char *const *paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes,
                    sf_block_sig *out, uint64_t cap, uint64_t *first_row, uint8_t *blocks_hashes,
                    uint64_t *n_out, uint32_t *bad_file);

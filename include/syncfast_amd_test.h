@@ -28,11 +28,7 @@ int sf_test_get_knob(const char* name, int64_t* value);
  *   "pages_locked"      caller ranges the library page-locked (hipHostRegister)
  *   "not_anon_refused"  caller ranges it did not page-lock because they are not
  *                       private anonymous memory (a file mapping, shared
- *                       memory): those are copied through the pinned stages;
- *   "chain_recovered"   stages of sf_index_files whose device blocks_hash
- *                       lanes gave up waiting (SF_ETIMEDOUT): their
- *                       blocks_hash values were computed on the host from
- *                       the stage's (complete) digests instead. */
+ *                       memory): those are copied through the pinned stages. */
 int sf_test_get_stat(const char* name, int64_t* value);
 
 /* The processing order sha1_table_kernel gets for a sorted explicit list:

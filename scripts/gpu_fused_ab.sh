@@ -1,0 +1,6 @@
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out/fused
+timeout -k 10 300 python -u -m pytest -x -q -p no:cacheprovider --timeout 150 --timeout-method thread tests/test_gpu_robustness.py tests/test_gpu_files.py > gpurun_out/fused/tests.log 2>&1 || { echo tests failed; tail -20 gpurun_out/fused/tests.log; exit 1; }
+tail -2 gpurun_out/fused/tests.log
+REPS=6 timeout -k 10 600 python scripts/pool_ab.py nowait=syncfast_amd/lib/libsyncfast_amd.so fused=build_ab/fused/libsyncfast_amd.so > gpurun_out/fused/ab.log 2>&1 || { echo ab failed; tail -5 gpurun_out/fused/ab.log; exit 1; }
+cat gpurun_out/fused/ab.log

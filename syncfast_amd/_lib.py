@@ -193,7 +193,7 @@ def set_knob(name: str, value: int) -> int:
 
 def get_stat(name: str) -> int:
     """A route counter of the host entry points ("pages_locked",
-    "not_anon_refused", "chain_recovered")."""
+    "not_anon_refused")."""
     v = ctypes.c_int64()
     check(lib().sf_test_get_stat(name.encode(), ctypes.byref(v)), name)
     return v.value

@@ -196,7 +196,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
   rc = res.streams(streams, done);
   struct Buf {
     void* p;
-  } ddata[2], ddig[2], dfh[2], pin[2], pdig[2], pfh[2], dstat, pstat;
+  } ddata[2], ddig[2], dfh[2], pin[2], pdig[2], pfh[2];
   for (int i = 0; i < 2 && rc == SF_OK; i++) {
     rc = res.dev(i, max_bytes, &ddata[i].p);
     if (rc == SF_OK) rc = res.dev(3 + i, max_rows * 20, &ddig[i].p);
@@ -205,36 +205,26 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
     if (rc == SF_OK) rc = res.pin(3 + i, max_rows * 20, &pdig[i].p);
     if (rc == SF_OK) rc = res.pin(5 + i, max_files * 20, &pfh[i].p);
   }
-  if (rc == SF_OK) rc = res.dev(7, 2 * 16, &dstat.p);  // one int32 status per stage buffer, 16 B apart
-  if (rc == SF_OK) rc = res.pin(7, 2 * 16, &pstat.p);
   if (rc != SF_OK) return rc;
-  auto stat_dev = [&](int b) { return reinterpret_cast<int*>(static_cast<uint8_t*>(dstat.p) + 16 * b); };
-  auto stat_host = [&](int b) { return *reinterpret_cast<volatile int*>(static_cast<uint8_t*>(pstat.p) + 16 * b); };
   // Per stage: each file's blocks_hash from a device chain (one lane per
-  // file, in the batch launch) while the runs are short; on the host (SHA-NI
-  // over the digests, in harvest) once the longest run would keep a lone
-  // chain lane busy past the stage's copy.  A chain costs ~1.1 us per 64 B of
-  // digests: 128 MiB files (640 KiB runs) took 11.6 ms per 256 MiB stage,
-  // against 4.7 ms of PCIe (scripts/map_min_probe.py).
+  // file, after the stage's blocks) while the runs are short; on the host
+  // (SHA-NI over the digests, in harvest) once the longest run would keep a
+  // lone chain lane busy past the stage's copy.  A chain costs ~1.1 us per
+  // 64 B of digests: 128 MiB files (640 KiB runs) took 11.6 ms per 256 MiB
+  // stage, against 4.7 ms of PCIe (scripts/map_min_probe.py).
+  // The batch call gets no status word, so it takes the path that never
+  // waits (block kernel, then chain kernel; sf_index_device_batch): the
+  // chains are hidden behind the next stage's copy either way, and the fused
+  // launch's bounded wait -- which gave up once in round 5 -- is not on this
+  // route at all.
   constexpr uint64_t kDevChainMaxRun = 192u << 10;
   std::vector<char> dev_bh(stages.size(), 1);
   for (size_t k = 0; k < stages.size(); k++)
     for (uint32_t f : stages[k].files)
       if ((first_row[f + 1] - first_row[f]) * 20 > kDevChainMaxRun) dev_bh[k] = 0;
-  // A stage whose device blocks_hash lanes gave up waiting (SF_ETIMEDOUT, a
-  // backstop never expected: sha1_staged_kernel) still has every digest --
-  // the launch finished before the D2H -- so its blocks_hash values are
-  // computed on the host instead (counted: "chain_recovered").  Seen once in
-  // round 5 (profiles/r05/pool/ab_2.log), never reproduced.
-  auto harvest = [&](size_t k) {  // SF_OK, or an unknown device status
+  auto harvest = [&](size_t k) {
     const FileStage& st = stages[k];
     const int b = (int)(k & 1);
-    bool host_bh = !dev_bh[k];
-    if (dev_bh[k] && stat_host(b) != SF_OK) {
-      if (stat_host(b) != SF_ETIMEDOUT) return stat_host(b);
-      host_bh = true;
-      stat_add(S_CHAIN_RECOVERED);
-    }
     const uint8_t* dg = static_cast<const uint8_t*>(pdig[b].p);
     const uint8_t* fh = static_cast<const uint8_t*>(pfh[b].p);
     uint64_t r = 0;
@@ -247,7 +237,7 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
         o[i].size = (uint32_t)std::min<uint64_t>(bs, size[f] - i * bs);
         memcpy(o[i].sha1, dg + 20 * r, 20);
       }
-      if (!host_bh) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
+      if (dev_bh[k]) memcpy(blocks_hashes + 20ull * f, fh + 20 * j, 20);
       else sf_host_sha1_impl(dg + 20 * (r - nb), nb * 20, blocks_hashes + 20ull * f, 0);
     }
     return SF_OK;
@@ -273,15 +263,11 @@ static int sf_index_files_body(const char* const* paths, uint32_t n_files, uint3
       break;
     }
     uint64_t nb = 0;
-    if (dev_bh[k] && hipMemsetAsync(stat_dev(b), 0, sizeof(int), s) != hipSuccess) { rc = SF_ENODEV; break; }
     rc = sf_index_device_batch(ddata[b].p, st.bytes, st.desc.data(), (uint32_t)st.files.size(), bs, ddig[b].p,
-                               max_rows, dev_bh[k] ? dfh[b].p : nullptr, nullptr, &nb,
-                               dev_bh[k] ? stat_dev(b) : nullptr, s);
+                               max_rows, dev_bh[k] ? dfh[b].p : nullptr, nullptr, &nb, nullptr, s);
     if (rc) break;
     if ((nb && hipMemcpyAsync(pdig[b].p, ddig[b].p, nb * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         (dev_bh[k] && hipMemcpyAsync(pfh[b].p, dfh[b].p, st.files.size() * 20, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-        (dev_bh[k] && hipMemcpyAsync(static_cast<uint8_t*>(pstat.p) + 16 * b, stat_dev(b), sizeof(int),
-                                     hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipEventRecord(done[b], s) != hipSuccess) {
       rc = SF_ENODEV;
       break;

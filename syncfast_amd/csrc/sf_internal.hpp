@@ -60,11 +60,9 @@ extern std::atomic<int64_t> g_knob[K_COUNT];
 inline int64_t knob(Knob k) { return g_knob[k].load(std::memory_order_relaxed); }
 
 // Counters of the routes the host entry points took (read by the tests
-// through sf_test_get_stat): pages the library page-locked, ranges it
-// refused to page-lock because they are not private anonymous memory, and
-// stages of sf_index_files whose device blocks_hash lanes gave up waiting
-// (SF_ETIMEDOUT) and whose blocks_hash values were computed on the host.
-enum Stat { S_PAGES_LOCKED, S_NOT_ANON_REFUSED, S_CHAIN_RECOVERED, S_COUNT };
+// through sf_test_get_stat): pages the library page-locked, and ranges it
+// refused to page-lock because they are not private anonymous memory.
+enum Stat { S_PAGES_LOCKED, S_NOT_ANON_REFUSED, S_COUNT };
 extern std::atomic<int64_t> g_stat[S_COUNT];
 inline void stat_add(Stat s, int64_t v = 1) { g_stat[s].fetch_add(v, std::memory_order_relaxed); }
 
@@ -163,7 +161,7 @@ struct HostRes {
   hipEvent_t ev[2] = {nullptr, nullptr};
   // Slots (device and pinned alike): 0, 1 = the two stages; 2 = the digest
   // table of one file; 3, 4 = the digest tables of sf_index_files' two
-  // stages; 5, 6 = their blocks_hash arrays; 7 = their status words.
+  // stages; 5, 6 = their blocks_hash arrays; 7 = unused.
   static constexpr int kSlots = 8;
   void* dev[kSlots] = {};
   uint64_t dev_cap[kSlots] = {};

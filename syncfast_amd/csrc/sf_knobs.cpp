@@ -47,7 +47,7 @@ void read_hook(uint64_t window) {
   const sf_test_read_hook_fn fn = g_read_hook.load(std::memory_order_acquire);
   if (fn) fn(g_read_hook_arg.load(std::memory_order_relaxed), window);
 }
-static const char* const kStatNames[S_COUNT] = {"pages_locked", "not_anon_refused", "chain_recovered"};
+static const char* const kStatNames[S_COUNT] = {"pages_locked", "not_anon_refused"};
 
 namespace {
 struct LoadKnobs {
