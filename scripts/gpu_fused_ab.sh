@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 A/B: sf_index_files on the non-waiting batch path (in-tree build) vs
 # the fused launch with its bounded wait (build_ab/fused: the library built
-# from commit 8c3dbd0 or earlier, see scripts/gpu_pool_ab.sh for the recipe).
+# from commit b53f593, see scripts/gpu_pool_ab.sh for the recipe).
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/fused
 timeout -k 10 300 python -u -m pytest -x -q -p no:cacheprovider --timeout 150 --timeout-method thread tests/test_gpu_robustness.py tests/test_gpu_files.py > gpurun_out/fused/tests.log 2>&1 || { echo tests failed; tail -20 gpurun_out/fused/tests.log; exit 1; }
