@@ -251,7 +251,7 @@ def _code_objects(path: str):
 
 FIXED_KERNEL = "_ZN2sf17sha1_fixed_kernelILi128ELi1ELb0EEEvPKhmjmPhNS_11PadScheduleEPj"
 CHAINED_KERNEL = "_ZN2sf25sha1_fixed_chained_kernelILi128EEEvPKhmjmPhNS_11PadScheduleENS_8ChainJobES5_jjj"
-TABLE_KERNEL = "_ZN2sf17sha1_table_kernelILi128ELb0EEEvPKhmPKmPKjmPhPiPjS6_S9_"
+TABLE_KERNEL = "_ZN2sf17sha1_table_kernelILi128ELb0EEEvPKhmPKmPKjmPhPiPjS6_"
 
 
 def kernel_code_sha256(path: str = None, symbol: str = FIXED_KERNEL) -> str:

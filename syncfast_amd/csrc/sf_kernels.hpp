@@ -853,20 +853,16 @@ __device__ __forceinline__ void table_group(const uint8_t* __restrict__ data, ui
 //     the sort's order the same SIMDs would start with every round's
 //     longest group.  Round 1 therefore takes its groups in reverse (below):
 //     SIMD work max/mean 1.07 -> 1.047, the CDC-like list 2 % faster.
-// next_group: unused (kept in the signature until the list kernel's next
-// form replaces it).
 template <int TILE, bool WEAK = false>
 __global__ void __launch_bounds__(64 * kTableWG, kTableWavesPerSimd)
 sha1_table_kernel(const uint8_t* __restrict__ data, uint64_t len, const uint64_t* __restrict__ offsets,
                   const uint32_t* __restrict__ sizes, uint64_t nblocks, uint8_t* __restrict__ digests,
-                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order,
-                  uint32_t* __restrict__ next_group) {
+                  int* __restrict__ status, uint32_t* __restrict__ weak, const uint32_t* __restrict__ order) {
   constexpr int kWaveTile = 64 * (TILE / 16) > 64 * kListPieces ? 64 * (TILE / 16) : 64 * kListPieces;
   __shared__ uint4 smem[kTableWG * kWaveTile];
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint4* tile = smem + wid * kWaveTile;
   const uint32_t ngroups = (uint32_t)((nblocks + 63) / 64);  // <= 2^25: the launcher splits at 2^31 blocks
-  (void)next_group;
   uint32_t g = blockIdx.x * kTableWG + wid;
   // The first rounds of waves land one per SIMD per round (wave w and
   // w + kTableRound on the same SIMD, traces of round 4), so in the sort's

@@ -18,14 +18,13 @@ int launch_table_kernel(bool weak_form, const uint8_t* d_data, uint64_t len, con
                         const uint32_t* order, hipStream_t stream) {
   const uint64_t ngroups = (nblocks + 63) / 64;
   const unsigned grid = (unsigned)((ngroups + sf::kTableWG - 1) / sf::kTableWG);
-  uint32_t* const next_group = nullptr;
   sfi::clear_stale_error();
   if (weak_form)
     hipLaunchKernelGGL((sf::sha1_table_kernel<128, true>), dim3(grid), dim3(64 * sf::kTableWG), 0, stream, d_data, len,
-                       d_offsets, d_sizes, nblocks, d_digests, d_status, weak, order, next_group);
+                       d_offsets, d_sizes, nblocks, d_digests, d_status, weak, order);
   else
     hipLaunchKernelGGL((sf::sha1_table_kernel<128, false>), dim3(grid), dim3(64 * sf::kTableWG), 0, stream, d_data, len,
-                       d_offsets, d_sizes, nblocks, d_digests, d_status, nullptr, order, next_group);
+                       d_offsets, d_sizes, nblocks, d_digests, d_status, nullptr, order);
   return hip_err(hipGetLastError());
 }
 
