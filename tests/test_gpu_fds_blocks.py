@@ -310,3 +310,40 @@ def test_index_path_default_mode_on_the_gpu(gpu, tmp_path, threads):
             np.zeros((0, 20), np.uint8)
         assert [h.bytes for h, _o, _s in rows] == [bytes(d) for d in dig], n
         assert bh.bytes == oracle.blocks_hash(dig) and idx.compute_blocks_hash(fid) == bh, n
+
+
+def _odd_list(n, rng):
+    """An allowed but unusual list over an n-byte file: sorted offsets, gaps,
+    overlaps, empty blocks, blocks up to the end."""
+    k = int(rng.integers(0, 40))
+    offs = np.sort(rng.integers(0, n + 1, k)).astype(np.uint64) if n else np.zeros(k, np.uint64)
+    sizes = np.array([int(rng.integers(0, n - o + 1)) if n > o else 0 for o in offs], np.uint32)
+    return offs, sizes
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fds_fuzz(gpu, tmp_path, seed):
+    """Seeded random calls: 1-40 files of 0 B .. 2 MiB, each with a CDC-like,
+    4 KiB fixed-like or odd list, stage sizes from 64 KiB to 4 MiB, with and
+    without stamps; every row and blocks_hash against the oracle."""
+    rng = np.random.default_rng(7900 + seed)
+    nf = int(rng.integers(1, 41))
+    files = []
+    for k in range(nf):
+        n = int(rng.choice([0, 1, int(rng.integers(2, 70_000)), int(rng.integers(70_000, 2 * MIB))]))
+        data = oracle.splitmix_bytes(n, 8000 + 100 * seed + k).tobytes() if n else b""
+        p = tmp_path / f"z{k:03d}"
+        p.write_bytes(data)
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            sizes = _cdc_like_sizes(n, 9000 + 100 * seed + k, mean=int(rng.choice([512, 8192])))
+            offs = _offs(sizes)
+        elif kind == 1:
+            offs = np.arange(0, n, 4096, dtype=np.uint64)
+            sizes = np.minimum(4096, n - offs).astype(np.uint32)
+        else:
+            offs, sizes = _odd_list(n, rng)
+        files.append((p, data, offs, sizes))
+    stage = int(rng.choice([64 * KIB, 300 * KIB, 1 * MIB, 4 * MIB]))
+    rows, first, hashes, status = _run(files, stamps=bool(rng.integers(0, 2)), stage_bytes=stage)
+    _check(files, rows, first, hashes, status)
