@@ -5,7 +5,8 @@ cache.  One line per run: tree, -j, SF_IO_THREADS, -S, wall, hash call, wait.
 
 usage: python scripts/default_mode_sweep.py [j,j,...] [io,io,...] [S,S,...] [reps]
 FORMS=base,base+G64,...: forms interleaved within each setting; +G64 passes
--G 64 (stages of 64 MiB inside each sf_index_fds_blocks call); FORM@DIR runs
+-G 64 (stages of 64 MiB inside each sf_index_fds_blocks call), +S64 -S 64
+(64 MiB batches, after the S of the setting); FORM@DIR runs
 the consumer against DIR/libsyncfast_amd.so (LD_LIBRARY_PATH before its
 RUNPATH).  (Round 5 also measured a batch plan that ramped the first and
 last batches down, with no gain: removed)
@@ -58,8 +59,8 @@ def main():
                     env["LD_LIBRARY_PATH"] = os.path.abspath(form.split("@", 1)[1])
                 if os.environ.get("TRACE") == "1":
                     env["SF_TRACE"] = "1"
-                plan = form.split("@")[0].split("+")  # "base+G64": 64 MiB stages per call
-                flags = [a for g in plan[1:] for a in ("-G", g[1:])]
+                plan = form.split("@")[0].split("+")  # "base+G64": 64 MiB stages per call; "+S64": 64 MiB batches
+                flags = [a for g in plan[1:] for a in (("-S" if g[0] == "S" else "-G"), g[1:])]
                 r = subprocess.run([EXE, "-Z", "-M", "-q", "-T", "-P", "2", "-j", str(j), "-S", str(S)] + flags + paths,
                                    capture_output=True, text=True, env=env, timeout=300)
                 if r.returncode:
