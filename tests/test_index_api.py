@@ -608,3 +608,40 @@ def test_index_file_that_keeps_changing_falls_back_to_one_pass(tmp_path, monkeyp
     assert b"".join(data[o:o + s] for _h, o, s in rows) == data
     assert all(hashlib.sha1(data[o:o + s]).digest() == h.bytes for h, o, s in rows)
     assert idx.compute_blocks_hash(fid) == bh
+
+
+def test_index_path_stream_chunker_property(tmp_path, monkeypatch):
+    """Property (hypothesis, seeded): for random trees (nested directories,
+    files of 0 B .. 40 KB), batch sizes and chunker thread counts, the
+    default mode's many-file pipeline (the oracle standing in for the device
+    call) stores exactly what the file-by-file path stores: the same files
+    in the same order, the same rows in the same order, the same
+    blocks_hash."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    _oracle_device_calls(monkeypatch)
+    counter = [0]
+
+    @settings(max_examples=15, deadline=None, derandomize=True,
+              suppress_health_check=[HealthCheck.function_scoped_fixture])
+    @given(sizes=st.lists(st.integers(0, 40_000), min_size=1, max_size=25),
+           depth=st.lists(st.integers(0, 2), min_size=25, max_size=25),
+           batch=st.sampled_from([1, 5_000, 60_000, 1 << 30]), threads=st.integers(1, 4))
+    def check(sizes, depth, batch, threads):
+        counter[0] += 1
+        root = tmp_path / f"t{counter[0]}"
+        for k, n in enumerate(sizes):
+            d = root.joinpath(*[f"d{j}" for j in range(depth[k])])
+            d.mkdir(parents=True, exist_ok=True)
+            (d / f"f{k:02d}").write_bytes(oracle.splitmix_bytes(n, 9500 + k).tobytes())
+        got = Index.open_in_memory(chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
+        got.index_path(root, batch_bytes=batch, chunk_threads=threads)
+        ref = Index.open_in_memory(chunker=BoundaryChunker(_stream_toy_cdc, stream=True))
+        ref.index_path(root, batch_bytes=0)
+        for q in ("SELECT file_id, name, blocks_hash FROM files ORDER BY file_id",
+                  "SELECT file_id, hash, offset, size, present FROM blocks ORDER BY rowid"):
+            assert got.db.execute(q).fetchall() == ref.db.execute(q).fetchall()
+
+    check()
+    assert counter[0] >= 10  # the examples ran
