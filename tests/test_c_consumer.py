@@ -209,3 +209,19 @@ def test_c_consumer_default_mode_many_files(gpu, tmp_path, threads):
         dig = oracle.index_blocks(d, offs, sizes) if sizes.size else np.zeros((0, 20), np.uint8)
         assert got[p]["rows"] == [(int(o), int(s), bytes(h).hex()) for o, s, h in zip(offs, sizes, dig)], p
         assert got[p]["bh"] == oracle.blocks_hash(dig).hex(), p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bs", [((5 << 20) + 123, 4096), (1, 4096), (0, 4096), (777_777, 1000)])
+def test_c_consumer_one_file_on_every_device(gpu, tmp_path, n, bs):
+    # -X 0: sf_index_file_multi on every visible device (one here): the
+    # oracle's rows and blocks_hash, from plain C
+    exe = _built(False)
+    data = oracle.splitmix_bytes(n, 41)
+    p = tmp_path / "m.bin"
+    data.tofile(p)
+    r = subprocess.run([exe, "-X", "0", "-b", str(bs), str(p)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = _parse(r.stdout)[str(p)]
+    rows, bh = _want(data, bs)
+    assert got["rows"] == rows and got["bh"] == bh
