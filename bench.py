@@ -298,20 +298,30 @@ def config1_default_mode_e2e():
         raw = oracle.splitmix_bytes(CONFIG1_BYTES, SEED).tobytes()
         with open(path, "wb") as f:
             f.write(raw)
-        r = subprocess.run([exe, "-Z", "-T", path, path, path], capture_output=True, text=True, timeout=300)
-        if r.returncode != 0:
-            return {"status": f"sf_index -Z failed ({r.returncode}): {r.stderr.strip()[-300:]}"}
-        times = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")]
-        rows = []
-        for ln in r.stdout.splitlines():
-            parts = ln.split()
-            if len(parts) == 3 and parts[0].isdigit():
-                rows.append((int(parts[0]), int(parts[1]), parts[2]))
-        nb = times[-1]["blocks"]
-        last = rows[-nb:]
-        assert sum(s for _o, s, _h in last) == CONFIG1_BYTES, "e2e rows do not tile the file"
-        for o, s, h in random.Random(7).sample(last, min(16, len(last))):
-            assert host.sha1(np.frombuffer(raw[o:o + s], np.uint8)).hex() == h, "e2e row self-check failed"
+        def run(extra):
+            r = subprocess.run([exe, "-Z", "-T"] + extra + [path, path, path], capture_output=True, text=True,
+                               timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"sf_index -Z {' '.join(extra)} failed ({r.returncode}): {r.stderr.strip()[-300:]}")
+            times = [json.loads(ln) for ln in r.stderr.splitlines() if ln.startswith("{")]
+            rows = []
+            for ln in r.stdout.splitlines():
+                parts = ln.split()
+                if len(parts) == 3 and parts[0].isdigit():
+                    rows.append((int(parts[0]), int(parts[1]), parts[2]))
+            last = rows[-times[-1]["blocks"]:]
+            assert sum(s for _o, s, _h in last) == CONFIG1_BYTES, "e2e rows do not tile the file"
+            for o, s, h in random.Random(7).sample(last, min(16, len(last))):
+                assert host.sha1(np.frombuffer(raw[o:o + s], np.uint8)).hex() == h, "e2e row self-check failed"
+            return times, last
+        try:
+            times, last = run([])
+            ptimes, plast = run(["-p", str(CONFIG1_CUT_THREADS)])
+        except RuntimeError as e:
+            return {"status": str(e)}
+        # the parallel cut is the one-stream cut: same rows, row for row
+        assert plast == last, "sf_cut_fd's boundaries differ from the one-stream cut"
+        nb = len(last)
     finally:
         try:
             os.unlink(path)
@@ -320,14 +330,25 @@ def config1_default_mode_e2e():
         os.rmdir(d)
     best = min(times[1:] or times, key=lambda t: t["chunk_s"] + t["hash_s"])
     c, h = best["chunk_s"], best["hash_s"]
+    pbest = min(ptimes[1:] or ptimes, key=lambda t: t["chunk_s"] + t["hash_s"])
+    pc, ph = pbest["chunk_s"], pbest["hash_s"]
     return {"bytes": CONFIG1_BYTES, "blocks": nb, "passes": len(times),
             "chunker_GB/s": round(CONFIG1_BYTES / c / 1e9, 4), "hash_call_GB/s": round(CONFIG1_BYTES / h / 1e9, 3),
             "e2e_GB/s": round(CONFIG1_BYTES / (c + h) / 1e9, 4), "chunker_share": round(c / (c + h), 4),
             "route": "file (page cache) -> stand-in chunker over the open fd (1 host core, 64 KiB reads) -> "
                      "sf_index_fd_blocks on the same fd (pread windows, H2D, sha1_table_kernel, D2H rows + "
                      "blocks_hash)",
+            "parallel_cut": {"threads": CONFIG1_CUT_THREADS, "chunker_GB/s": round(CONFIG1_BYTES / pc / 1e9, 4),
+                             "hash_call_GB/s": round(CONFIG1_BYTES / ph / 1e9, 3),
+                             "e2e_GB/s": round(CONFIG1_BYTES / (pc + ph) / 1e9, 4),
+                             "chunker_share": round(pc / (pc + ph), 4), "rows_equal_one_stream": True,
+                             "route": "the same file cut by sf_cut_fd (the stand-in chunker on "
+                                      f"{CONFIG1_CUT_THREADS} threads, segments joined to the one-stream "
+                                      "boundaries) -> sf_index_fd_blocks on the same fd"},
             "label": "stand-in chunker: the crate's per-byte work, not its boundaries"}
 
+
+CONFIG1_CUT_THREADS = 16  # the box's CPU share per GPU
 
 DEFAULT_MODE_TREES = {
     # config 3's shape: 1024 files of 8 MiB (BASELINE configs[2]); a tree of 0-200 KiB files

@@ -259,6 +259,63 @@ static double now_s(void) {
  * of zpaq_standin.h (the crate's per-byte work, not its boundaries).  -T: one
  * line per file on stderr, {"zpaq_file": ..., "bytes", "blocks", "chunk_s",
  * "hash_s"}: the host chunker's time and the hashing call's. */
+/* The stand-in chunker as sf_chunker_ops (sf_cut_fd calls it from the
+ * library's threads, one chunker per thread). */
+static void *zpaq_create(void *ctx) {
+    (void)ctx;
+    sf_zpaq *z = malloc(sizeof *z);
+    if (z) sf_zpaq_init(z, 13, 32768); /* ZPAQ_BITS, MAX_BLOCK_SIZE: src/index.rs:40-41 */
+    return z;
+}
+static size_t zpaq_next(void *ch, const uint8_t *p, size_t n) { return sf_zpaq_next(ch, p, n); }
+static void zpaq_destroy(void *ch) { free(ch); }
+
+/* -Z -p N: index_zpaq with the file cut by sf_cut_fd on N threads (the
+ * boundaries are the one-stream cut's, whatever N), then hashed from the same
+ * descriptor by sf_index_fd_blocks. */
+static int index_zpaq_parallel(const char *path, uint32_t threads, int timing) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return SF_EIO;
+    const sf_chunker_ops ops = {zpaq_create, zpaq_next, zpaq_destroy, NULL};
+    uint64_t *offs = NULL, n = 0;
+    uint32_t *sizes = NULL;
+    sf_block_sig *rows = NULL;
+    uint8_t bh[20];
+    double t_chunk = 0, t_hash = 0;
+    int rc = SF_EAGAIN;
+    for (int attempt = 0; attempt < 3 && rc == SF_EAGAIN; attempt++) { /* a file written meanwhile: again */
+        sf_file_stamp st;
+        if ((rc = sf_file_stamp_fd(fd, &st)) != SF_OK) break;
+        sf_free_cuts(offs);
+        sf_free_cuts(sizes);
+        offs = NULL;
+        sizes = NULL;
+        const double t0 = now_s();
+        rc = sf_cut_fd(fd, &st, &ops, threads, &offs, &sizes, &n);
+        t_chunk = now_s() - t0;
+        if (rc != SF_OK) continue;
+        free(rows);
+        if (!(rows = malloc((n ? n : 1) * sizeof(sf_block_sig)))) { rc = SF_ENOMEM; break; }
+        const double t1 = now_s();
+        rc = sf_index_fd_blocks(fd, &st, offs, sizes, n, rows, bh);
+        t_hash = now_s() - t1;
+    }
+    close(fd);
+    if (rc == SF_OK) {
+        print_rows(path, rows, n, bh);
+        if (timing) {
+            uint64_t total = n ? offs[n - 1] + sizes[n - 1] : 0;
+            fprintf(stderr, "{\"zpaq_file\": \"%s\", \"threads\": %u, \"bytes\": %llu, \"blocks\": %llu, "
+                            "\"chunk_s\": %.6f, \"hash_s\": %.6f}\n",
+                    path, threads, (unsigned long long)total, (unsigned long long)n, t_chunk, t_hash);
+        }
+    }
+    sf_free_cuts(offs);
+    sf_free_cuts(sizes);
+    free(rows);
+    return rc;
+}
+
 static int index_zpaq(const char *path, int timing) {
     enum { kRead = 1 << 16 };
     const int fd = open(path, O_RDONLY);
@@ -723,7 +780,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
-    int passes = 1, multi = -1;
+    int passes = 1, multi = -1, cut_threads = -1;
     uint64_t batch_mib = 256, stage_mib = 0;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
@@ -734,6 +791,7 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-v") == 0) wire_cdc = atoll(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-j") == 0) threads = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-X") == 0) multi = atoi(argv[++i]);
+        else if (i + 1 < argc && strcmp(argv[i], "-p") == 0) cut_threads = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
         else if (i + 1 < argc && strcmp(argv[i], "-G") == 0) stage_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
@@ -748,7 +806,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-p cut_threads] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -796,6 +854,7 @@ int main(int argc, char **argv) {
     }
     for (; i < argc; i++) {
         const int rc = multi >= 0 ? index_multi(argv[i], bs, multi)
+                       : (zpaq && cut_threads >= 0) ? index_zpaq_parallel(argv[i], (uint32_t)cut_threads, timing)
                        : zpaq  ? index_zpaq(argv[i], timing)
                        : cdc ? index_cdc(argv[i])
                        : (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)

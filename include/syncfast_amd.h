@@ -32,6 +32,7 @@
 #ifndef SYNCFAST_AMD_H
 #define SYNCFAST_AMD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -397,6 +398,49 @@ int sf_index_fds_blocks(const int *fds, const sf_file_stamp *stamps, uint32_t n_
                         const uint64_t *const *offsets, const uint32_t *const *sizes, const uint64_t *n_blocks,
                         uint64_t stage_bytes, sf_block_sig *out, uint64_t cap, uint64_t *first_row,
                         uint8_t *blocks_hashes, int *file_status, uint32_t *bad_file);
+
+/* -------------------------------- the caller's chunker, on N threads ---- */
+
+/* A content-defined chunker of the caller's (cdchunking's ZPAQ with its
+ * max_size cap, src/index.rs:622-625, on the Rust side), as three functions:
+ *   create(ctx)       a fresh chunker: the state at a chunk's first byte;
+ *   next(ch, p, n)    feeds p[0, n): the number of bytes up to and including
+ *                     the next boundary, or 0 if the chunk goes on past p + n;
+ *                     after a boundary the state is a fresh chunk's again;
+ *   destroy(ch).
+ * The chunker must restart at every boundary (its state after a boundary is a
+ * fresh chunker's, which read_block relies on, src/sync/fs.rs:26-40): then
+ * the boundaries are a function of where a chunk starts, which is what lets
+ * sf_cut_fd cut one file on several threads and still return exactly the
+ * sequential boundaries.  Called from the library's threads, one chunker
+ * per thread at a time. */
+typedef struct sf_chunker_ops {
+    void *(*create)(void *ctx);
+    size_t (*next)(void *chunker, const uint8_t *p, size_t n);
+    void (*destroy)(void *chunker);
+    void *ctx;
+} sf_chunker_ops;
+
+/* The boundaries of the regular file open on fd (pread only; the position is
+ * not used), cut by `ops`, exactly as one chunker streaming the file from its
+ * first byte would cut it (the loop of src/index.rs:629-647 without the
+ * SHA-1).  With threads > 1 (0 = the library's reader count) the file is
+ * split into up to `threads` segments of at least 1 MiB; a chunker starts
+ * fresh at each segment's first byte and cuts speculatively; the segments are
+ * then joined left to right: from the last boundary known to be right, the
+ * file is cut again on one thread only until a boundary coincides with one of
+ * the next segment's, after which (the chunker restarting at every boundary)
+ * the two agree.  The result never depends on the thread count.  *offsets /
+ * *sizes (n_blocks entries; allocated by the library, release both with
+ * sf_free_cuts) are the blocks in file order; an empty file has none.
+ * expect (may be NULL): the caller's sf_file_stamp_fd; the file's stamp is
+ * compared with it at the start and with the one taken at the start after the
+ * last read: SF_EAGAIN if it changed (cut it again).  SF_EINVAL if fd is not
+ * a regular file or ops is incomplete, SF_EIO on a failed or short read,
+ * SF_ENOMEM.  Host only (no device).  Blocking. */
+int sf_cut_fd(int fd, const sf_file_stamp *expect, const sf_chunker_ops *ops, uint32_t threads,
+              uint64_t **offsets, uint32_t **sizes, uint64_t *n_blocks);
+void sf_free_cuts(void *p);
 
 /* ------------------------------------------- one process, N devices ---- */
 

@@ -261,6 +261,30 @@ def index_fds_blocks(fds: Sequence[int], lists: Sequence[Tuple[object, object]],
     return out[:total], first, hashes[:n], status[:n]
 
 
+def cut_fd(fd: int, ops, threads: int = 0, stamp: FileStamp = None) -> Tuple[np.ndarray, np.ndarray]:
+    """The caller's chunker over the regular file open on fd (sf_cut_fd):
+    ``ops`` is the address of an sf_chunker_ops (a native chunker; see
+    examples/zpaq_standin_ops.c).  Split over ``threads`` threads (0: the
+    library's reader count) and joined so that the boundaries are exactly the
+    sequential ones.  Returns (offsets uint64, sizes uint32); raises
+    SfError(SF_EAGAIN) if the file changed (against ``stamp`` if given, and
+    while it was cut)."""
+    po, pz = ctypes.c_void_p(), ctypes.c_void_p()
+    n = ctypes.c_uint64(0)
+    check(lib().sf_cut_fd(fd, ctypes.byref(stamp) if stamp is not None else None, ops, threads,
+                          ctypes.byref(po), ctypes.byref(pz), ctypes.byref(n)), "sf_cut_fd")
+    try:
+        k = n.value
+        offs = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_uint64)), (k,)).copy() if k else \
+            np.zeros(0, np.uint64)
+        sizes = np.ctypeslib.as_array(ctypes.cast(pz, ctypes.POINTER(ctypes.c_uint32)), (k,)).copy() if k else \
+            np.zeros(0, np.uint32)
+    finally:
+        lib().sf_free_cuts(po)
+        lib().sf_free_cuts(pz)
+    return offs, sizes
+
+
 def shard_range(file_len: int, block_size: int, n_shards: int, shard: int) -> Tuple[int, int]:
     """sf_shard_range: (start, length) of shard `shard` of n_shards (the
     partition of the multi-device forms)."""

@@ -225,3 +225,30 @@ def test_c_consumer_one_file_on_every_device(gpu, tmp_path, n, bs):
     got = _parse(r.stdout)[str(p)]
     rows, bh = _want(data, bs)
     assert got["rows"] == rows and got["bh"] == bh
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [2, 16])
+def test_c_consumer_parallel_cut(gpu, tmp_path, threads):
+    # -Z -p N: the stand-in chunker over each file on N threads (sf_cut_fd),
+    # then sf_index_fd_blocks: every row equals the one-stream cut's (the
+    # oracle's stand-in over the whole file) with the oracle's digests
+    exe = _built(False)
+    files = {}
+    for i, n in enumerate([0, 1, 70_000, (9 << 20) + 5, (33 << 20) + 77]):
+        data = oracle.splitmix_bytes(n, 950 + i)
+        p = tmp_path / f"p{i}"
+        data.tofile(p)
+        files[str(p)] = data
+    z = np.zeros(12 << 20, np.uint8)  # the size cap and a degenerate hash across segment edges
+    z.tofile(tmp_path / "zeros")
+    files[str(tmp_path / "zeros")] = z
+    r = subprocess.run([exe, "-Z", "-p", str(threads)] + list(files), capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    got = _parse(r.stdout.decode())
+    for name, data in files.items():
+        sizes = oracle.zpaq_standin_sizes(data).astype(np.uint64)
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) if sizes.size else sizes
+        dig = oracle.index_blocks(data, offs, sizes.astype(np.uint32)) if sizes.size else np.zeros((0, 20), np.uint8)
+        rows = [(int(o), int(s), bytes(d).hex()) for o, s, d in zip(offs, sizes, dig)]
+        assert got[name]["rows"] == rows and got[name]["bh"] == oracle.blocks_hash(dig).hex(), name
