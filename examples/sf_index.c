@@ -270,9 +270,41 @@ static void *zpaq_create(void *ctx) {
 static size_t zpaq_next(void *ch, const uint8_t *p, size_t n) { return sf_zpaq_next(ch, p, n); }
 static void zpaq_destroy(void *ch) { free(ch); }
 
-/* -Z -p N: index_zpaq with the file cut by sf_cut_fd on N threads (the
- * boundaries are the one-stream cut's, whatever N), then hashed from the same
- * descriptor by sf_index_fd_blocks. */
+/* -Z -p N: index_zpaq with the chunker on N threads: sf_index_fd_cut (the
+ * file read once, cut by sf_cut_fd's segments and join -- the one-stream
+ * boundaries whatever N -- and hashed from the copy already in HBM). */
+static int index_zpaq_fused(const char *path, uint32_t threads, int timing) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return SF_EIO;
+    const sf_chunker_ops ops = {zpaq_create, zpaq_next, zpaq_destroy, NULL};
+    sf_block_sig *rows = NULL;
+    uint64_t n = 0;
+    uint8_t bh[20];
+    int rc = SF_EAGAIN;
+    double t = 0;
+    for (int attempt = 0; attempt < 3 && rc == SF_EAGAIN; attempt++) { /* a file written meanwhile: again */
+        sf_free_rows(rows);
+        rows = NULL;
+        const double t0 = now_s();
+        rc = sf_index_fd_cut(fd, NULL, &ops, threads, &rows, &n, bh);
+        t = now_s() - t0;
+    }
+    close(fd);
+    if (rc == SF_OK) {
+        print_rows(path, rows, n, bh);
+        if (timing) {
+            const uint64_t total = n ? rows[n - 1].offset + rows[n - 1].size : 0;
+            fprintf(stderr, "{\"zpaq_file\": \"%s\", \"threads\": %u, \"bytes\": %llu, \"blocks\": %llu, "
+                            "\"chunk_s\": 0, \"hash_s\": %.6f, \"fused\": 1}\n",
+                    path, threads, (unsigned long long)total, (unsigned long long)n, t);
+        }
+    }
+    sf_free_rows(rows);
+    return rc;
+}
+
+/* -Z -p N -W: the same as two calls -- sf_cut_fd on N threads, then
+ * sf_index_fd_blocks hashing the list from the descriptor (a second read). */
 static int index_zpaq_parallel(const char *path, uint32_t threads, int timing) {
     const int fd = open(path, O_RDONLY);
     if (fd < 0) return SF_EIO;
@@ -780,7 +812,7 @@ static int index_many(char **paths, int n, uint32_t bs) {
 int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
-    int passes = 1, multi = -1, cut_threads = -1;
+    int passes = 1, multi = -1, cut_threads = -1, two_calls = 0;
     uint64_t batch_mib = 256, stage_mib = 0;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
@@ -792,6 +824,7 @@ int main(int argc, char **argv) {
         else if (i + 1 < argc && strcmp(argv[i], "-j") == 0) threads = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-X") == 0) multi = atoi(argv[++i]);
         else if (i + 1 < argc && strcmp(argv[i], "-p") == 0) cut_threads = atoi(argv[++i]);
+        else if (strcmp(argv[i], "-W") == 0) two_calls = 1;
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
         else if (i + 1 < argc && strcmp(argv[i], "-G") == 0) stage_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
@@ -806,7 +839,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-p cut_threads] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-p cut_threads [-W]] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -854,7 +887,8 @@ int main(int argc, char **argv) {
     }
     for (; i < argc; i++) {
         const int rc = multi >= 0 ? index_multi(argv[i], bs, multi)
-                       : (zpaq && cut_threads >= 0) ? index_zpaq_parallel(argv[i], (uint32_t)cut_threads, timing)
+                       : (zpaq && cut_threads >= 0 && two_calls) ? index_zpaq_parallel(argv[i], (uint32_t)cut_threads, timing)
+                       : (zpaq && cut_threads >= 0) ? index_zpaq_fused(argv[i], (uint32_t)cut_threads, timing)
                        : zpaq  ? index_zpaq(argv[i], timing)
                        : cdc ? index_cdc(argv[i])
                        : (buffer || shards > 0) ? index_buffer_or_shards(argv[i], bs, buffer ? 0 : shards)

@@ -442,6 +442,19 @@ int sf_cut_fd(int fd, const sf_file_stamp *expect, const sf_chunker_ops *ops, ui
               uint64_t **offsets, uint32_t **sizes, uint64_t *n_blocks);
 void sf_free_cuts(void *p);
 
+/* index_file (src/index.rs:610-659) in the default mode for one regular file
+ * open on fd, with the caller's chunker on several threads: the boundaries
+ * of sf_cut_fd (exactly the one-stream ones) and every block's SHA-1 and the
+ * blocks_hash on the device, with the file read ONCE: each segment is read
+ * into a pinned copy of the file by the thread that cuts it, copied to HBM
+ * while the segments are cut and joined, and the joined list is hashed from
+ * there.  A file larger than 512 MiB is cut (sf_cut_fd) and then hashed from
+ * its descriptor (sf_index_fd_blocks).  *rows (n_out entries, allocated by
+ * the library, release with sf_free_rows) and blocks_hash as sf_index_fd_blocks
+ * gives them.  expect / SF_EAGAIN / errors as sf_cut_fd.  Blocking. */
+int sf_index_fd_cut(int fd, const sf_file_stamp *expect, const sf_chunker_ops *ops, uint32_t threads,
+                    sf_block_sig **rows, uint64_t *n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]);
+
 /* ------------------------------------------- one process, N devices ---- */
 
 /* Contiguous, block-aligned shard `shard` of n_shards of a file_len-byte file:

@@ -51,7 +51,8 @@ run lookup -L -b 4096 "$W"/f09 "$W"/f09 || rc=1
 run cdc -C "$W"/f0* || rc=1
 run zpaq -Z "$W"/f0* || rc=1  # default splice: stamp + stand-in chunker + sf_index_fd_blocks
 # the default mode over many files: chunker threads + sf_index_fds_blocks, 1 MiB batches, two passes
-run zpaq_par -Z -p 4 "$W"/f0* || rc=1  # the file cut by sf_cut_fd on 4 threads
+run zpaq_par -Z -p 4 "$W"/f0* || rc=1  # the file cut on 4 threads, read once, hashed from HBM (sf_index_fd_cut)
+run zpaq_par2 -Z -p 4 -W "$W"/f0* || rc=1  # sf_cut_fd, then sf_index_fd_blocks
 run zpaq_many -Z -M -j 4 -S 1 -P 2 "$W"/f0* || rc=1
 run zpaq_many_small -Z -M -j 4 -S 1 "$W"/s* || rc=1
 run multi -X 0 -b 4096 "$W"/f0* || rc=1  # one file on every visible device from one process
@@ -60,6 +61,7 @@ run wire_cdc -v 20000001 || rc=1
 same() { [ -s "$1" ] && cmp -s "$1" "$2"; }  # equal, and not two empty outputs
 same "$W/zpaq.asan" "$W/zpaq_many.asan" && echo "zpaq_many == zpaq: ok" || { echo "zpaq_many differs from zpaq"; rc=1; }
 same "$W/zpaq.asan" "$W/zpaq_par.asan" && echo "zpaq_par == zpaq: ok" || { echo "zpaq_par differs from zpaq"; rc=1; }
+same "$W/zpaq.asan" "$W/zpaq_par2.asan" && echo "zpaq_par2 == zpaq: ok" || { echo "zpaq_par2 differs from zpaq"; rc=1; }
 for m in buffer shards inplace inplace_bounce multi; do
   same "$W/files.asan" "$W/$m.asan" && echo "$m == files: ok" || { echo "$m differs from files"; rc=1; }
 done

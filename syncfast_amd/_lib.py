@@ -34,7 +34,7 @@ EXPORTED = (
     "sf_index_device_fixed_weak", "sf_index_device_blocks_weak", "sf_index_device_batch_chained",
     "sf_index_device_batch_chained_cols",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_file_stamp_fd", "sf_index_fd_blocks", "sf_index_fd_fixed", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
-    "sf_index_fds_blocks", "sf_cut_fd", "sf_free_cuts", "sf_shard_range", "sf_index_file_multi",
+    "sf_index_fds_blocks", "sf_cut_fd", "sf_free_cuts", "sf_index_fd_cut", "sf_shard_range", "sf_index_file_multi",
     "sf_index_device_multi",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
@@ -132,6 +132,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_cut_fd.argtypes = [i32, vp, vp, u32, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]
     L.sf_free_cuts.argtypes = [vp]
     L.sf_free_cuts.restype = None
+    L.sf_index_fd_cut.argtypes = [i32, vp, vp, u32, ctypes.POINTER(ctypes.POINTER(BlockSig)), pu64, vp]
     L.sf_shard_range.argtypes = [u64, u32, u32, u32, pu64, pu64]
     L.sf_index_file_multi.argtypes = [ctypes.c_char_p, u32, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
     L.sf_index_device_multi.argtypes = [u32, vp, u64, u32, vp, u32, vp, vp]

@@ -21,7 +21,9 @@
 // matched, so the result is the sequential one for any thread count; the
 // parallel part only saves time when the chains meet early, which for a
 // chunker whose state is a hash of recent bytes happens within a few chunks.
-// Host only: no HIP call.
+// sf_index_fd_cut adds the hashing: every segment is read once into a pinned
+// copy of the file, copied to HBM while it is being cut, and the joined list
+// is hashed from there (sha1_table_kernel) -- no second read of the file.
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -34,6 +36,7 @@
 #include <functional>
 #include <vector>
 
+#include "host_sha1.h"
 #include "sf_internal.hpp"
 
 using namespace sfi;
@@ -54,27 +57,36 @@ struct Chunker {
   Chunker& operator=(const Chunker&) = delete;
 };
 
+// Bytes [pos, pos + want) of the file: read into `buf` (pread), or a pointer
+// into memory that already holds them.  nullptr: a read failed or came short.
+using Fetch = std::function<const uint8_t*(uint64_t pos, uint64_t want, uint8_t* buf)>;
+
+const uint8_t* pread_fetch(int fd, uint64_t pos, uint64_t want, uint8_t* buf) {
+  for (uint64_t got = 0; got < want;) {
+    const ssize_t r = pread(fd, buf + got, want - got, (off_t)(pos + got));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return nullptr;  // an error, or the file shrank below len
+    got += (uint64_t)r;
+  }
+  return buf;
+}
+
 // Cuts the file from `start` (a chunk's first byte) with a fresh chunker and
 // calls on_end(end) for each chunk's end (the end of the file included, for a
 // last chunk that no boundary closes) until it returns false or the file
 // ends.  SF_OK, SF_EIO (a read failed or came short of len), SF_EINVAL (the
 // chunker answered more bytes than it was given), SF_ENOMEM.
-int cut_from(int fd, uint64_t len, const sf_chunker_ops* ops, uint64_t start, std::vector<uint8_t>& buf,
+int cut_from(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint64_t start, std::vector<uint8_t>& buf,
              const std::function<bool(uint64_t)>& on_end) {
   Chunker c(ops);
   if (!c.ch) return SF_ENOMEM;
   uint64_t pos = start, last = start;
   while (pos < len) {
     const uint64_t want = std::min<uint64_t>(kPiece, len - pos);
-    uint64_t got = 0;
-    while (got < want) {
-      const ssize_t r = pread(fd, buf.data() + got, want - got, (off_t)(pos + got));
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0) return SF_EIO;  // an error, or the file shrank below len
-      got += (uint64_t)r;
-    }
+    const uint8_t* p = fetch(pos, want, buf.data());
+    if (!p) return SF_EIO;
     for (uint64_t q = 0; q < want;) {
-      const size_t k = ops->next(c.ch, buf.data() + q, (size_t)(want - q));
+      const size_t k = ops->next(c.ch, p + q, (size_t)(want - q));
       if (k == 0) break;
       if (k > want - q) return SF_EINVAL;
       q += k;
@@ -84,6 +96,81 @@ int cut_from(int fd, uint64_t len, const sf_chunker_ops* ops, uint64_t start, st
     pos += want;
   }
   if (last < len) on_end(len);  // the last chunk ends with the file
+  return SF_OK;
+}
+
+// The file's segments and the join (the file comment): `fetch` supplies the
+// bytes, `seg_begin(i)` runs on the thread that takes segment i before it is
+// cut (the fused route reads the segment and starts its copy there).  The
+// true chain's ends go to `ends`.
+int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint32_t threads,
+               const std::function<int(uint64_t, uint64_t, uint64_t)>& seg_begin, std::vector<uint64_t>& ends) {
+  ends.clear();
+  if (!len) return SF_OK;
+  const uint64_t want = threads ? threads : io_threads();
+  const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(want, len / kMinSeg));
+  std::vector<uint64_t> P(k + 1);
+  for (uint64_t i = 0; i <= k; i++) P[i] = len / k * i;
+  P[k] = len;
+  // 1. every segment's speculative chain, up to its first end at or past the
+  // next segment's start (segment 0's is true: it starts at byte 0)
+  std::vector<std::vector<uint64_t>> C(k);
+  std::vector<int> rcs(k, SF_OK);
+  std::atomic<uint64_t> next{0};
+  run_pool((unsigned)k, [&] {
+    std::vector<uint8_t> buf(kPiece);
+    for (uint64_t i; (i = next.fetch_add(1)) < k;) {
+      if ((rcs[i] = seg_begin(i, P[i], P[i + 1])) != SF_OK) continue;
+      const uint64_t stop = P[i + 1];
+      std::vector<uint64_t>& out = C[i];
+      rcs[i] = cut_from(fetch, len, ops, P[i], buf, [&](uint64_t e) {
+        out.push_back(e);
+        return e < stop;
+      });
+    }
+  });
+  for (int rc : rcs)
+    if (rc != SF_OK) return rc;
+  // 2. join left to right
+  ends = std::move(C[0]);
+  std::vector<uint8_t> buf(kPiece);
+  for (uint64_t i = 1; i < k && ends.back() < len; i++) {
+    const std::vector<uint64_t>& Ci = C[i];
+    const uint64_t L = ends.back();
+    auto in_ci = [&](uint64_t e) { return std::binary_search(Ci.begin(), Ci.end(), e); };
+    // a true end already known past P[i] that the segment's chain has too
+    bool synced = false;
+    for (auto it = std::upper_bound(ends.begin(), ends.end(), P[i]); it != ends.end(); ++it)
+      if (in_ci(*it)) {
+        synced = true;
+        break;
+      }
+    if (synced) {
+      ends.insert(ends.end(), std::upper_bound(Ci.begin(), Ci.end(), L), Ci.end());
+      continue;
+    }
+    // otherwise cut again from L until an end is one of the segment's, or
+    // the segment's chain is passed
+    const uint64_t c_last = Ci.empty() ? 0 : Ci.back();
+    uint64_t met = 0;
+    const int rc = cut_from(fetch, len, ops, L, buf, [&](uint64_t e) {
+      ends.push_back(e);
+      if (in_ci(e)) {
+        met = e;
+        return false;
+      }
+      return e < c_last;
+    });
+    if (rc != SF_OK) return rc;
+    if (met) ends.insert(ends.end(), std::upper_bound(Ci.begin(), Ci.end(), met), Ci.end());
+  }
+  // the last segment's chain may stop short of the file's end only if every
+  // segment was joined by re-cutting: finish the chain
+  if (ends.back() < len)
+    return cut_from(fetch, len, ops, ends.back(), buf, [&](uint64_t e) {
+      ends.push_back(e);
+      return true;
+    });
   return SF_OK;
 }
 
@@ -105,78 +192,11 @@ static int sf_cut_fd_body(int fd, const sf_file_stamp* expect, const sf_chunker_
   if (expect && !same_stamp(before, *expect)) return SF_EAGAIN;
   const uint64_t len = before.size;
   std::vector<uint64_t> ends;  // the true chain: every chunk's end, in order
-  if (len) {
-    const uint64_t want = threads ? threads : io_threads();
-    const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(want, len / kMinSeg));
-    std::vector<uint64_t> P(k + 1);
-    for (uint64_t i = 0; i <= k; i++) P[i] = len / k * i;
-    P[k] = len;
-    // 1. every segment's speculative chain, up to its first end at or past
-    // the next segment's start (segment 0's is true: it starts at byte 0)
-    std::vector<std::vector<uint64_t>> C(k);
-    std::vector<int> rcs(k, SF_OK);
-    std::atomic<uint64_t> next{0};
-    run_pool((unsigned)k, [&] {
-      std::vector<uint8_t> buf(kPiece);
-      for (uint64_t i; (i = next.fetch_add(1)) < k;) {
-        const uint64_t stop = P[i + 1];
-        std::vector<uint64_t>& out = C[i];
-        rcs[i] = cut_from(fd, len, ops, P[i], buf, [&](uint64_t e) {
-          out.push_back(e);
-          return e < stop;
-        });
-      }
-    });
-    for (int rc : rcs)
-      if (rc != SF_OK) {
-        if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) return SF_EAGAIN;
-        return rc;
-      }
-    // 2. join left to right
-    ends = std::move(C[0]);
-    std::vector<uint8_t> buf(kPiece);
-    for (uint64_t i = 1; i < k && ends.back() < len; i++) {
-      const std::vector<uint64_t>& Ci = C[i];
-      const uint64_t L = ends.back();
-      auto in_ci = [&](uint64_t e) { return std::binary_search(Ci.begin(), Ci.end(), e); };
-      // a true end already known past P[i] that the segment's chain has too
-      bool synced = false;
-      for (auto it = std::upper_bound(ends.begin(), ends.end(), P[i]); it != ends.end(); ++it)
-        if (in_ci(*it)) {
-          synced = true;
-          break;
-        }
-      if (synced) {
-        ends.insert(ends.end(), std::upper_bound(Ci.begin(), Ci.end(), L), Ci.end());
-        continue;
-      }
-      // otherwise cut again from L until an end is one of the segment's, or
-      // the segment's chain is passed
-      const uint64_t c_last = Ci.empty() ? 0 : Ci.back();
-      uint64_t met = 0;
-      const int rc = cut_from(fd, len, ops, L, buf, [&](uint64_t e) {
-        ends.push_back(e);
-        if (in_ci(e)) {
-          met = e;
-          return false;
-        }
-        return e < c_last;
-      });
-      if (rc != SF_OK) {
-        if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) return SF_EAGAIN;
-        return rc;
-      }
-      if (met) ends.insert(ends.end(), std::upper_bound(Ci.begin(), Ci.end(), met), Ci.end());
-    }
-    // the last segment's chain may stop short of the file's end only if
-    // every segment was joined by re-cutting: finish the chain
-    if (ends.back() < len) {
-      const int rc = cut_from(fd, len, ops, ends.back(), buf, [&](uint64_t e) {
-        ends.push_back(e);
-        return true;
-      });
-      if (rc != SF_OK) return rc;
-    }
+  const Fetch fetch = [fd](uint64_t pos, uint64_t want, uint8_t* buf) { return pread_fetch(fd, pos, want, buf); };
+  const int rc = cut_joined(fetch, len, ops, threads, [](uint64_t, uint64_t, uint64_t) { return SF_OK; }, ends);
+  if (rc != SF_OK) {
+    if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) return SF_EAGAIN;
+    return rc;
   }
   if (!stamp_of(fd, &after, nullptr)) return SF_EIO;
   if (!same_stamp(before, after)) return SF_EAGAIN;  // written while cut: not one version's boundaries
@@ -209,5 +229,133 @@ int sf_cut_fd(int fd, const sf_file_stamp* expect, const sf_chunker_ops* ops, ui
 }
 
 void sf_free_cuts(void* p) { free(p); }
+
+// The fused form takes files up to this size in one pinned copy (the host
+// cache's largest buffer); a larger file is cut (sf_cut_fd) and then hashed
+// from its descriptor by windows (sf_index_fd_blocks).
+static constexpr uint64_t kFusedMax = 512ull << 20;
+
+static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_chunker_ops* ops, uint32_t threads,
+                                sf_block_sig** rows, uint64_t* n_out, uint8_t* blocks_hash) {
+  if (rows) *rows = nullptr;
+  if (n_out) *n_out = 0;
+  if (fd < 0 || !ops || !ops->create || !ops->next || !ops->destroy || !rows || !n_out || !blocks_hash)
+    return SF_EINVAL;
+  sf_file_stamp before{}, after{};
+  mode_t mode = 0;
+  if (!stamp_of(fd, &before, &mode)) return SF_EIO;
+  if (!S_ISREG(mode)) return SF_EINVAL;
+  if (expect && !same_stamp(before, *expect)) return SF_EAGAIN;
+  const uint64_t len = before.size;
+  if (len > kFusedMax) {  // cut, then hash from the descriptor
+    uint64_t *o = nullptr, n = 0;
+    uint32_t* z = nullptr;
+    int rc = sf_cut_fd_body(fd, &before, ops, threads, &o, &z, &n);
+    if (rc != SF_OK) return rc;
+    sf_block_sig* out = static_cast<sf_block_sig*>(malloc((n ? n : 1) * sizeof(sf_block_sig)));
+    rc = out ? sf_index_fd_blocks(fd, &before, o, z, n, out, blocks_hash) : SF_ENOMEM;
+    free(o);
+    free(z);
+    if (rc != SF_OK) {
+      free(out);
+      return rc;
+    }
+    *rows = out;
+    *n_out = n;
+    return SF_OK;
+  }
+  int dev = 0;
+  SF_HIP(hipGetDevice(&dev));
+  HostLease res;
+  hipStream_t* st;
+  hipEvent_t* done_ev;
+  uint8_t *pin = nullptr, *dfile = nullptr;
+  int rc = res.streams(st, done_ev);
+  if (rc == SF_OK) rc = res.pin(0, len, reinterpret_cast<void**>(&pin));
+  if (rc == SF_OK) rc = res.dev(0, len, reinterpret_cast<void**>(&dfile));
+  if (rc != SF_OK) return rc;
+  // 1. cut: each segment read once into the pinned copy and its copy to HBM
+  // started by the thread that took it, then cut from there; a chunk running
+  // past the segment reads on with pread until the next segment is in
+  const uint64_t nseg_max = 4096;
+  std::vector<std::atomic<int>> seg_in(nseg_max);
+  for (auto& a : seg_in) a.store(0, std::memory_order_relaxed);
+  // cut_joined's segments: k of len / k bytes, the last one longer by the rest
+  const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(threads ? threads : io_threads(), len / kMinSeg));
+  const uint64_t seg_len = std::max<uint64_t>(1, len / k);
+  auto seg_of = [&](uint64_t pos) { return std::min<uint64_t>(pos / seg_len, k - 1); };
+  const Fetch fetch = [&](uint64_t pos, uint64_t want, uint8_t* buf) -> const uint8_t* {
+    bool in = true;
+    for (uint64_t j = seg_of(pos); in && j <= seg_of(pos + want - 1); j++)
+      in = seg_in[j].load(std::memory_order_acquire) == 1;
+    return in ? pin + pos : pread_fetch(fd, pos, want, buf);
+  };
+  const auto seg_begin = [&](uint64_t i, uint64_t a, uint64_t b) -> int {
+    if (i >= nseg_max || i >= k || a != i * seg_len) return SF_EINVAL;  // the plan must be cut_joined's
+    if (!pread_fetch(fd, a, b - a, pin + a)) return SF_EIO;
+    if (hipSetDevice(dev) != hipSuccess ||
+        hipMemcpyAsync(dfile + a, pin + a, b - a, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
+      (void)hipGetLastError();
+      return SF_ENODEV;
+    }
+    seg_in[i].store(1, std::memory_order_release);
+    return SF_OK;
+  };
+  std::vector<uint64_t> ends;
+  rc = cut_joined(fetch, len, ops, threads, seg_begin, ends);
+  if (rc == SF_OK && !stamp_of(fd, &after, nullptr)) rc = SF_EIO;
+  if (rc == SF_OK && !same_stamp(before, after)) rc = SF_EAGAIN;  // written while read: not one version's rows
+  if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
+  if (rc != SF_OK) return rc;
+  // 2. hash: the joined list, one launch over the file's bytes already in HBM
+  const uint64_t n = ends.size();
+  sf_block_sig* out = static_cast<sf_block_sig*>(malloc((n ? n : 1) * sizeof(sf_block_sig)));
+  if (!out) return SF_ENOMEM;
+  struct Free {
+    sf_block_sig*& p;
+    ~Free() { free(p); }
+  } guard{out};
+  uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
+  if (n) {
+    const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
+    if ((rc = res.pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
+        (rc = res.dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
+        (rc = res.pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
+        (rc = res.dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
+      return rc;
+    uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
+    uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);
+    for (uint64_t j = 0, b = 0; j < n; b = ends[j], j++) {
+      if (ends[j] - b > 0xFFFFFFFFull) return SF_EINVAL;
+      lo[j] = b;
+      lz[j] = (uint32_t)(ends[j] - b);
+    }
+    SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[0]));
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(dlist);
+    if ((rc = launch_table(dfile, len, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
+                           st[0])) != SF_OK)
+      return rc;
+    SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[0]));
+    SF_HIP(hipStreamSynchronize(st[0]));
+    for (uint64_t j = 0; j < n; j++) {
+      out[j].offset = lo[j];
+      out[j].size = lz[j];
+      memcpy(out[j].sha1, pdig + 20 * j, 20);
+    }
+  } else {
+    SF_HIP(hipStreamSynchronize(st[0]));
+  }
+  static const uint8_t kNone[1] = {0};
+  sf_host_sha1_impl(n ? pdig : kNone, n * 20, blocks_hash, 0);  // compute_blocks_hash (src/index.rs:661-682)
+  *rows = out;
+  *n_out = n;
+  guard.p = nullptr;
+  return SF_OK;
+}
+
+int sf_index_fd_cut(int fd, const sf_file_stamp* expect, const sf_chunker_ops* ops, uint32_t threads,
+                    sf_block_sig** rows, uint64_t* n_out, uint8_t blocks_hash[SF_HASH_DIGEST_LEN]) {
+  return guarded([&] { return sf_index_fd_cut_body(fd, expect, ops, threads, rows, n_out, blocks_hash); });
+}
 
 }  // extern "C"

@@ -285,6 +285,25 @@ def cut_fd(fd: int, ops, threads: int = 0, stamp: FileStamp = None) -> Tuple[np.
     return offs, sizes
 
 
+def index_fd_cut(fd: int, ops, threads: int = 0, stamp: FileStamp = None) -> Tuple[np.ndarray, bytes]:
+    """index_file in the default mode for the regular file open on fd, the
+    caller's chunker (``ops``: the address of an sf_chunker_ops) on
+    ``threads`` threads, the file read once (sf_index_fd_cut).  Returns
+    (rows, blocks_hash); SfError(SF_EAGAIN) if the file changed."""
+    p = ctypes.POINTER(BlockSig)()
+    n = ctypes.c_uint64(0)
+    bh = (ctypes.c_uint8 * 20)()
+    check(lib().sf_index_fd_cut(fd, ctypes.byref(stamp) if stamp is not None else None, ops, threads,
+                                ctypes.byref(p), ctypes.byref(n), bh), "sf_index_fd_cut")
+    try:
+        rows = np.zeros(n.value, SIG_DTYPE)
+        if n.value:
+            ctypes.memmove(rows.ctypes.data, p, n.value * SIG_DTYPE.itemsize)
+    finally:
+        lib().sf_free_rows(p)
+    return rows, bytes(bh)
+
+
 def shard_range(file_len: int, block_size: int, n_shards: int, shard: int) -> Tuple[int, int]:
     """sf_shard_range: (start, length) of shard `shard` of n_shards (the
     partition of the multi-device forms)."""

@@ -228,11 +228,13 @@ def test_c_consumer_one_file_on_every_device(gpu, tmp_path, n, bs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [2, 16])
-def test_c_consumer_parallel_cut(gpu, tmp_path, threads):
-    # -Z -p N: the stand-in chunker over each file on N threads (sf_cut_fd),
-    # then sf_index_fd_blocks: every row equals the one-stream cut's (the
-    # oracle's stand-in over the whole file) with the oracle's digests
+@pytest.mark.parametrize("threads,two_calls", [(2, False), (16, False), (16, True)])
+def test_c_consumer_parallel_cut(gpu, tmp_path, threads, two_calls):
+    # -Z -p N: the stand-in chunker over each file on N threads, the file read
+    # once and hashed from HBM (sf_index_fd_cut); -W: sf_cut_fd, then
+    # sf_index_fd_blocks from the descriptor.  Every row equals the
+    # one-stream cut's (the oracle's stand-in over the whole file) with the
+    # oracle's digests
     exe = _built(False)
     files = {}
     for i, n in enumerate([0, 1, 70_000, (9 << 20) + 5, (33 << 20) + 77]):
@@ -243,7 +245,8 @@ def test_c_consumer_parallel_cut(gpu, tmp_path, threads):
     z = np.zeros(12 << 20, np.uint8)  # the size cap and a degenerate hash across segment edges
     z.tofile(tmp_path / "zeros")
     files[str(tmp_path / "zeros")] = z
-    r = subprocess.run([exe, "-Z", "-p", str(threads)] + list(files), capture_output=True, timeout=300)
+    r = subprocess.run([exe, "-Z", "-p", str(threads)] + (["-W"] if two_calls else []) + list(files),
+                       capture_output=True, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     got = _parse(r.stdout.decode())
     for name, data in files.items():

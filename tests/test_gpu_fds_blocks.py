@@ -347,3 +347,46 @@ def test_fds_fuzz(gpu, tmp_path, seed):
     stage = int(rng.choice([64 * KIB, 300 * KIB, 1 * MIB, 4 * MIB]))
     rows, first, hashes, status = _run(files, stamps=bool(rng.integers(0, 2)), stage_bytes=stage)
     _check(files, rows, first, hashes, status)
+
+
+def _standin_ops():
+    import ctypes
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "build",
+                      "libzpaq_standin.so")
+    assert os.path.exists(so), f"{so} not built: run __graft_entry__.build()"
+    lib = ctypes.CDLL(so)
+    lib.sf_zpaq_standin_ops.restype = ctypes.c_void_p
+    lib.sf_zpaq_standin_ops.argtypes = [ctypes.c_uint, ctypes.c_uint32]
+    lib.sf_zpaq_standin_ops_free.argtypes = [ctypes.c_void_p]
+    return lib, lib.sf_zpaq_standin_ops(13, 32768)
+
+
+@pytest.mark.parametrize("n", [0, 1, 70_000, (37 << 20) + 99, (600 << 20) + 5])
+def test_index_fd_cut_equals_oracle(gpu, tmp_path, n):
+    """sf_index_fd_cut: the stand-in chunker on 16 threads, the file read once
+    and hashed from HBM (a file over 512 MiB: cut, then hashed from its
+    descriptor); rows and blocks_hash equal the one-stream cut hashed by the
+    oracle, and a stale stamp is SF_EAGAIN."""
+    lib, ops = _standin_ops()
+    try:
+        data = oracle.splitmix_bytes(n, 7700 + n % 97)
+        p = tmp_path / "f"
+        data.tofile(p)
+        sizes = oracle.zpaq_standin_sizes(data).astype(np.uint32)
+        offs = _offs(sizes)
+        dig = oracle.index_blocks(data, offs, sizes) if sizes.size else np.zeros((0, 20), np.uint8)
+        with open(p, "rb") as f:
+            st = host.file_stamp(f.fileno())
+            rows, bh = host.index_fd_cut(f.fileno(), ops, 16, st)
+        assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes)
+        assert np.array_equal(rows["sha1"], dig) and bh == oracle.blocks_hash(dig)
+        if n > 1:
+            with open(p, "r+b") as g:
+                g.write(b"\x01")
+            os.utime(p, ns=(st.mtime_sec * 10**9 + st.mtime_nsec, st.mtime_sec * 10**9 + st.mtime_nsec + 1))
+            with open(p, "rb") as f:
+                with pytest.raises(_lib.SfError) as e:
+                    host.index_fd_cut(f.fileno(), ops, 16, st)
+            assert e.value.code == _lib.SF_EAGAIN
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)
