@@ -31,8 +31,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <stdio.h>
+
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <vector>
 
@@ -301,8 +304,12 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     seg_in[i].store(1, std::memory_order_release);
     return SF_OK;
   };
+  const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   std::vector<uint64_t> ends;
   rc = cut_joined(fetch, len, ops, threads, seg_begin, ends);
+  const double t_cut = ms();
   if (rc == SF_OK && !stamp_of(fd, &after, nullptr)) rc = SF_EIO;
   if (rc == SF_OK && !same_stamp(before, after)) rc = SF_EAGAIN;  // written while read: not one version's rows
   if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
@@ -336,7 +343,11 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
                            st[0])) != SF_OK)
       return rc;
     SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[0]));
+    const double t_issue = ms();
     SF_HIP(hipStreamSynchronize(st[0]));
+    if (trace)
+      fprintf(stderr, "sf_index_fd_cut trace: %llu B, %llu blocks: cut+join %.3f, list+issue %.3f, device wait %.3f ms\n",
+              (unsigned long long)len, (unsigned long long)n, t_cut, t_issue - t_cut, ms() - t_issue);
     for (uint64_t j = 0; j < n; j++) {
       out[j].offset = lo[j];
       out[j].size = lz[j];
