@@ -49,6 +49,7 @@ returns them for ``WHERE file_id = ?`` with no ORDER BY (src/index.rs:663-
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 import os
 import sqlite3
@@ -182,6 +183,64 @@ class BoundaryChunker:
     def __init__(self, fn: Callable, stream: bool = False):
         self.fn = fn
         self.stream = stream
+
+
+class _ChunkerOps(ctypes.Structure):
+    """sf_chunker_ops (include/syncfast_amd.h)."""
+    _fields_ = [("create", ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p)),
+                ("next", ctypes.CFUNCTYPE(ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)),
+                ("destroy", ctypes.CFUNCTYPE(None, ctypes.c_void_p)),
+                ("ctx", ctypes.c_void_p)]
+
+
+class NativeChunker(BoundaryChunker):
+    """The reference's mode with a native chunker: ``ops`` is the address of
+    an sf_chunker_ops (create / next / destroy in C: cdchunking's ZPAQ on the
+    Rust side; examples/zpaq_standin_ops.c here).  The
+    library runs it itself: Index.index_file cuts and hashes a file in one
+    call on ``threads`` threads, the file read once (sf_index_fd_cut, the
+    one-stream boundaries whatever the thread count); Index.index_path cuts
+    the files on its pool (sf_cut_fd, one thread per file) and hashes them
+    as batches (sf_index_fds_blocks)."""
+
+    def __init__(self, ops: int, threads: int = 0):
+        super().__init__(self._sizes, stream=True)
+        self.ops = int(ops)
+        self.threads = threads
+
+    def _sizes(self, f) -> List[int]:
+        if hasattr(f, "fileno"):
+            try:
+                fd = f.fileno()
+            except (OSError, ValueError):  # io.BytesIO: the bytes of one read
+                fd = None
+            if fd is not None:
+                return host.cut_fd(fd, self.ops, 1)[1].tolist()
+        return self._cut_bytes(f.read())
+
+    def _cut_bytes(self, raw: bytes) -> List[int]:
+        """The chunker over bytes in memory, driven from here through its
+        three functions (the one-pass fallback of index_file)."""
+        ops = _ChunkerOps.from_address(self.ops)
+        ch = ops.create(ops.ctx)
+        if not ch:
+            raise MemoryError("chunker create failed")
+        try:
+            buf = ctypes.create_string_buffer(raw, len(raw)) if raw else None
+            base = ctypes.addressof(buf) if buf is not None else 0
+            sizes, start, pos = [], 0, 0
+            while pos < len(raw):
+                k = ops.next(ch, base + pos, len(raw) - pos)
+                if k == 0:
+                    break
+                pos += k
+                sizes.append(pos - start)
+                start = pos
+            if start < len(raw):
+                sizes.append(len(raw) - start)
+            return sizes
+        finally:
+            ops.destroy(ch)
 
 
 def _sizes_ok(sizes, n: int) -> List[int]:
@@ -519,6 +578,8 @@ class Index:
                     native = host.index_fd_fixed(f.fileno(), ch.block_size, stamp)
                 else:  # a FIFO: read sequentially from this open, as File::open + read do
                     native = host.index_fd(f.fileno(), ch.block_size)
+            elif isinstance(ch, NativeChunker) and seekable and not one_pass:
+                native = host.index_fd_cut(f.fileno(), ch.ops, ch.threads, stamp)  # cut + hash, one read
             elif ch.stream and seekable and not one_pass:
                 sizes = [int(x) for x in ch.fn(f)]
                 if sum(sizes) != stamp.size and _stamp_moved(f.fileno(), stamp):

@@ -390,3 +390,34 @@ def test_index_fd_cut_equals_oracle(gpu, tmp_path, n):
             assert e.value.code == _lib.SF_EAGAIN
     finally:
         lib.sf_zpaq_standin_ops_free(ops)
+
+
+@pytest.mark.parametrize("batch", [0, 1 << 30])
+def test_index_native_chunker_on_the_gpu(gpu, tmp_path, batch):
+    """Index(chunker=NativeChunker(stand-in ops)): index_file through
+    sf_index_fd_cut (batch 0) or the walk through sf_cut_fd per file and
+    sf_index_fds_blocks (batched); every stored row and blocks_hash against
+    the oracle's one-stream stand-in."""
+    from syncfast_amd.index import Index, NativeChunker
+    lib, ops = _standin_ops()
+    try:
+        root = tmp_path / "t"
+        root.mkdir()
+        datas = {}
+        for k, n in enumerate([0, 1, 9_999, (5 << 20) + 1, (17 << 20) + 321]):
+            d = oracle.splitmix_bytes(n, 7800 + k)
+            (root / f"f{k}").write_bytes(d.tobytes())
+            datas[f"f{k}"] = d
+        idx = Index.open_in_memory(chunker=NativeChunker(ops, threads=16))
+        idx.index_path(root, batch_bytes=batch)
+        for name, d in datas.items():
+            fid, _, bh = idx.get_file(name)
+            rows = idx.list_file_blocks(fid)
+            sizes = oracle.zpaq_standin_sizes(d).astype(np.uint32)
+            offs = _offs(sizes)
+            dig = oracle.index_blocks(d, offs, sizes) if sizes.size else np.zeros((0, 20), np.uint8)
+            assert [(o, s) for _h, o, s in rows] == list(zip(offs.tolist(), sizes.tolist())), name
+            assert [h.to_sql() for h, _o, _s in rows] == [bytes(x).hex() for x in dig], name
+            assert bh.to_sql() == oracle.blocks_hash(dig).hex(), name
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)

@@ -645,3 +645,64 @@ def test_index_path_stream_chunker_property(tmp_path, monkeypatch):
 
     check()
     assert counter[0] >= 10  # the examples ran
+
+
+def _standin_ops_lib():
+    import ctypes
+    import subprocess as _sp
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "examples", "build", "libzpaq_standin.so")
+    if not os.path.exists(so):
+        _sp.check_call(["make", "-s", "-C", os.path.join(root, "examples"), "build/libzpaq_standin.so"])
+    lib = ctypes.CDLL(so)
+    lib.sf_zpaq_standin_ops.restype = ctypes.c_void_p
+    lib.sf_zpaq_standin_ops.argtypes = [ctypes.c_uint, ctypes.c_uint32]
+    lib.sf_zpaq_standin_ops_free.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+def test_native_chunker_matches_the_python_chunker(tmp_path, monkeypatch):
+    """Index with a NativeChunker (the stand-in's sf_chunker_ops): index_file
+    (sf_index_fd_cut: the library cuts on its threads -- really, sf_cut_fd is
+    host-only -- with the oracle standing in for the device's hashes),
+    index_path (one thread per file, batches through sf_index_fds_blocks),
+    and the one-pass fallback (the ops driven from Python over one read's
+    bytes) all store what a Python BoundaryChunker with the oracle's
+    one-stream stand-in stores."""
+    from syncfast_amd import host
+    from syncfast_amd.index import NativeChunker
+    _oracle_device_calls(monkeypatch)
+
+    def fd_cut(fd, ops, threads=0, stamp=None):
+        offs, sizes = host.cut_fd(fd, ops, threads, stamp)
+        raw = _pread_all(fd)
+        rows = np.zeros(offs.size, host.SIG_DTYPE)
+        rows["offset"], rows["size"] = offs, sizes
+        dig = oracle.index_blocks(np.frombuffer(raw, np.uint8), offs, sizes) if offs.size else np.zeros((0, 20), np.uint8)
+        rows["sha1"] = dig
+        return rows, oracle.blocks_hash(dig)
+
+    monkeypatch.setattr(host, "index_fd_cut", fd_cut)
+    lib = _standin_ops_lib()
+    ops = lib.sf_zpaq_standin_ops(13, 32768)
+    try:
+        root = tmp_path / "tree"
+        (root / "sub").mkdir(parents=True)
+        for k, n in enumerate([0, 1, 5000, 70_000, (9 << 20) + 3, 300_000]):
+            (root / ("sub" if k % 2 else ".") / f"f{k}").write_bytes(oracle.splitmix_bytes(n, 9700 + k).tobytes())
+        ref = Index.open_in_memory(chunker=BoundaryChunker(lambda raw: oracle.zpaq_standin_sizes(raw).tolist()))
+        ref.index_path(root, batch_bytes=0)
+        q_files = "SELECT file_id, name, blocks_hash FROM files ORDER BY file_id"
+        q_blocks = "SELECT file_id, hash, offset, size, present FROM blocks ORDER BY file_id, offset"
+        for batch in (0, 1 << 30):  # index_file per file (fused route), then the batched walk
+            got = Index.open_in_memory(chunker=NativeChunker(ops, threads=4))
+            got.index_path(root, batch_bytes=batch)
+            assert got.db.execute(q_files).fetchall() == ref.db.execute(q_files).fetchall(), batch
+            assert got.db.execute(q_blocks).fetchall() == ref.db.execute(q_blocks).fetchall(), batch
+        # the one-pass fallback cuts one read's bytes through the ops from Python
+        nc = NativeChunker(ops)
+        data = oracle.splitmix_bytes(200_000, 9800)
+        import io
+        assert nc.fn(io.BytesIO(data.tobytes())) == oracle.zpaq_standin_sizes(data).tolist()
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)
