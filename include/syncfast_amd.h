@@ -448,8 +448,8 @@ void sf_free_cuts(void *p);
  * blocks_hash on the device, with the file read ONCE: each segment is read
  * into a pinned copy of the file by the thread that cuts it, copied to HBM
  * while the segments are cut and joined, and the joined list is hashed from
- * there.  A file larger than 512 MiB is cut (sf_cut_fd) and then hashed from
- * its descriptor (sf_index_fd_blocks).  *rows (n_out entries, allocated by
+ * there -- by windows of up to 512 MiB, each ending at the last boundary
+ * inside it (the next window starts there).  *rows (n_out entries, allocated by
  * the library, release with sf_free_rows) and blocks_hash as sf_index_fd_blocks
  * gives them.  expect / SF_EAGAIN / errors as sf_cut_fd.  Blocking. */
 int sf_index_fd_cut(int fd, const sf_file_stamp *expect, const sf_chunker_ops *ops, uint32_t threads,

@@ -74,13 +74,14 @@ const uint8_t* pread_fetch(int fd, uint64_t pos, uint64_t want, uint8_t* buf) {
   return buf;
 }
 
-// Cuts the file from `start` (a chunk's first byte) with a fresh chunker and
-// calls on_end(end) for each chunk's end (the end of the file included, for a
-// last chunk that no boundary closes) until it returns false or the file
-// ends.  SF_OK, SF_EIO (a read failed or came short of len), SF_EINVAL (the
-// chunker answered more bytes than it was given), SF_ENOMEM.
-int cut_from(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint64_t start, std::vector<uint8_t>& buf,
-             const std::function<bool(uint64_t)>& on_end) {
+// Cuts bytes [start, len) with a fresh chunker (start is a chunk's first
+// byte) and calls on_end(end) for each chunk's end until it returns false or
+// the bytes run out; when len is the end of the file (eof), a last chunk that
+// no boundary closes ends there too.  SF_OK, SF_EIO (a read failed or came
+// short), SF_EINVAL (the chunker answered more bytes than it was given),
+// SF_ENOMEM.
+int cut_from(const Fetch& fetch, uint64_t len, bool eof, const sf_chunker_ops* ops, uint64_t start,
+             std::vector<uint8_t>& buf, const std::function<bool(uint64_t)>& on_end) {
   Chunker c(ops);
   if (!c.ch) return SF_ENOMEM;
   uint64_t pos = start, last = start;
@@ -98,23 +99,31 @@ int cut_from(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint64
     }
     pos += want;
   }
-  if (last < len) on_end(len);  // the last chunk ends with the file
+  if (eof && last < len) on_end(len);  // the last chunk ends with the file
   return SF_OK;
 }
 
-// The file's segments and the join (the file comment): `fetch` supplies the
-// bytes, `seg_begin(i)` runs on the thread that takes segment i before it is
-// cut (the fused route reads the segment and starts its copy there).  The
-// true chain's ends go to `ends`.
-int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint32_t threads,
+// Segments of bytes [A, B): k of (B - A) / k bytes, the last one longer by
+// the rest (the fused route plans its reads with the same rule).
+inline uint64_t seg_count(uint64_t A, uint64_t B, uint32_t threads) {
+  return std::max<uint64_t>(1, std::min<uint64_t>(threads ? threads : io_threads(), (B - A) / kMinSeg));
+}
+
+// The segments of bytes [A, B) and the join (the file comment); A is a true
+// boundary, and B the end of the file if eof.  `fetch` supplies the bytes,
+// `seg_begin(i, a, b)` runs on the thread that takes segment i = [a, b)
+// before it is cut (the fused route reads the segment and starts its copy
+// there).  The true chain's ends in (A, B] go to `ends`; without eof, only
+// the ends of chunks that a boundary closes inside [A, B).
+int cut_joined(const Fetch& fetch, uint64_t A, uint64_t B, bool eof, const sf_chunker_ops* ops, uint32_t threads,
                const std::function<int(uint64_t, uint64_t, uint64_t)>& seg_begin, std::vector<uint64_t>& ends) {
   ends.clear();
-  if (!len) return SF_OK;
-  const uint64_t want = threads ? threads : io_threads();
-  const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(want, len / kMinSeg));
+  if (B <= A) return SF_OK;
+  const uint64_t len = B;
+  const uint64_t k = seg_count(A, B, threads);
   std::vector<uint64_t> P(k + 1);
-  for (uint64_t i = 0; i <= k; i++) P[i] = len / k * i;
-  P[k] = len;
+  for (uint64_t i = 0; i <= k; i++) P[i] = A + (B - A) / k * i;
+  P[k] = B;
   // 1. every segment's speculative chain, up to its first end at or past the
   // next segment's start (segment 0's is true: it starts at byte 0)
   std::vector<std::vector<uint64_t>> C(k);
@@ -126,7 +135,7 @@ int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint
       if ((rcs[i] = seg_begin(i, P[i], P[i + 1])) != SF_OK) continue;
       const uint64_t stop = P[i + 1];
       std::vector<uint64_t>& out = C[i];
-      rcs[i] = cut_from(fetch, len, ops, P[i], buf, [&](uint64_t e) {
+      rcs[i] = cut_from(fetch, len, eof, ops, P[i], buf, [&](uint64_t e) {
         out.push_back(e);
         return e < stop;
       });
@@ -134,12 +143,14 @@ int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint
   });
   for (int rc : rcs)
     if (rc != SF_OK) return rc;
-  // 2. join left to right
+  // 2. join left to right (the true chain so far ends at L: A before its
+  // first end)
   ends = std::move(C[0]);
   std::vector<uint8_t> buf(kPiece);
-  for (uint64_t i = 1; i < k && ends.back() < len; i++) {
+  auto last_end = [&] { return ends.empty() ? A : ends.back(); };
+  for (uint64_t i = 1; i < k && last_end() < len; i++) {
     const std::vector<uint64_t>& Ci = C[i];
-    const uint64_t L = ends.back();
+    const uint64_t L = last_end();
     auto in_ci = [&](uint64_t e) { return std::binary_search(Ci.begin(), Ci.end(), e); };
     // a true end already known past P[i] that the segment's chain has too
     bool synced = false;
@@ -154,9 +165,9 @@ int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint
     }
     // otherwise cut again from L until an end is one of the segment's, or
     // the segment's chain is passed
-    const uint64_t c_last = Ci.empty() ? 0 : Ci.back();
+    const uint64_t c_last = Ci.empty() ? P[i + 1] : Ci.back();  // an empty chain: re-cut through its segment
     uint64_t met = 0;
-    const int rc = cut_from(fetch, len, ops, L, buf, [&](uint64_t e) {
+    const int rc = cut_from(fetch, len, eof, ops, L, buf, [&](uint64_t e) {
       ends.push_back(e);
       if (in_ci(e)) {
         met = e;
@@ -167,10 +178,10 @@ int cut_joined(const Fetch& fetch, uint64_t len, const sf_chunker_ops* ops, uint
     if (rc != SF_OK) return rc;
     if (met) ends.insert(ends.end(), std::upper_bound(Ci.begin(), Ci.end(), met), Ci.end());
   }
-  // the last segment's chain may stop short of the file's end only if every
-  // segment was joined by re-cutting: finish the chain
-  if (ends.back() < len)
-    return cut_from(fetch, len, ops, ends.back(), buf, [&](uint64_t e) {
+  // the chain may stop short of B when the last segments were joined by
+  // re-cutting: finish it
+  if (last_end() < len)
+    return cut_from(fetch, len, eof, ops, last_end(), buf, [&](uint64_t e) {
       ends.push_back(e);
       return true;
     });
@@ -196,7 +207,7 @@ static int sf_cut_fd_body(int fd, const sf_file_stamp* expect, const sf_chunker_
   const uint64_t len = before.size;
   std::vector<uint64_t> ends;  // the true chain: every chunk's end, in order
   const Fetch fetch = [fd](uint64_t pos, uint64_t want, uint8_t* buf) { return pread_fetch(fd, pos, want, buf); };
-  const int rc = cut_joined(fetch, len, ops, threads, [](uint64_t, uint64_t, uint64_t) { return SF_OK; }, ends);
+  const int rc = cut_joined(fetch, 0, len, true, ops, threads, [](uint64_t, uint64_t, uint64_t) { return SF_OK; }, ends);
   if (rc != SF_OK) {
     if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) return SF_EAGAIN;
     return rc;
@@ -233,9 +244,8 @@ int sf_cut_fd(int fd, const sf_file_stamp* expect, const sf_chunker_ops* ops, ui
 
 void sf_free_cuts(void* p) { free(p); }
 
-// The fused form takes files up to this size in one pinned copy (the host
-// cache's largest buffer); a larger file is cut (sf_cut_fd) and then hashed
-// from its descriptor by windows (sf_index_fd_blocks).
+// The fused form's window: a pinned copy of up to this many bytes of the file
+// (the host cache's largest buffer) and its copy in HBM.
 static constexpr uint64_t kFusedMax = 512ull << 20;
 
 static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_chunker_ops* ops, uint32_t threads,
@@ -250,117 +260,131 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   if (!S_ISREG(mode)) return SF_EINVAL;
   if (expect && !same_stamp(before, *expect)) return SF_EAGAIN;
   const uint64_t len = before.size;
-  if (len > kFusedMax) {  // cut, then hash from the descriptor
-    uint64_t *o = nullptr, n = 0;
-    uint32_t* z = nullptr;
-    int rc = sf_cut_fd_body(fd, &before, ops, threads, &o, &z, &n);
-    if (rc != SF_OK) return rc;
-    sf_block_sig* out = static_cast<sf_block_sig*>(malloc((n ? n : 1) * sizeof(sf_block_sig)));
-    rc = out ? sf_index_fd_blocks(fd, &before, o, z, n, out, blocks_hash) : SF_ENOMEM;
-    free(o);
-    free(z);
-    if (rc != SF_OK) {
-      free(out);
-      return rc;
-    }
-    *rows = out;
-    *n_out = n;
-    return SF_OK;
-  }
   int dev = 0;
   SF_HIP(hipGetDevice(&dev));
+  const int64_t wk = knob(K_TEST_CUT_WINDOW_MIB);  // test hook: small windows exercise the window seams
+  const uint64_t W = wk > 0 ? (uint64_t)wk << 20 : kFusedMax;
   HostLease res;
   hipStream_t* st;
   hipEvent_t* done_ev;
-  uint8_t *pin = nullptr, *dfile = nullptr;
+  uint8_t *pin = nullptr, *dwin = nullptr;
   int rc = res.streams(st, done_ev);
-  if (rc == SF_OK) rc = res.pin(0, len, reinterpret_cast<void**>(&pin));
-  if (rc == SF_OK) rc = res.dev(0, len, reinterpret_cast<void**>(&dfile));
+  if (rc == SF_OK) rc = res.pin(0, std::min(len, W), reinterpret_cast<void**>(&pin));
+  if (rc == SF_OK) rc = res.dev(0, std::min(len, W), reinterpret_cast<void**>(&dwin));
   if (rc != SF_OK) return rc;
-  // 1. cut: each segment read once into the pinned copy and its copy to HBM
-  // started by the thread that took it, then cut from there; a chunk running
-  // past the segment reads on with pread until the next segment is in
-  const uint64_t nseg_max = 4096;
-  std::vector<std::atomic<int>> seg_in(nseg_max);
-  for (auto& a : seg_in) a.store(0, std::memory_order_relaxed);
-  // cut_joined's segments: k of len / k bytes, the last one longer by the rest
-  const uint64_t k = std::max<uint64_t>(1, std::min<uint64_t>(threads ? threads : io_threads(), len / kMinSeg));
-  const uint64_t seg_len = std::max<uint64_t>(1, len / k);
-  auto seg_of = [&](uint64_t pos) { return std::min<uint64_t>(pos / seg_len, k - 1); };
-  const Fetch fetch = [&](uint64_t pos, uint64_t want, uint8_t* buf) -> const uint8_t* {
-    bool in = true;
-    for (uint64_t j = seg_of(pos); in && j <= seg_of(pos + want - 1); j++)
-      in = seg_in[j].load(std::memory_order_acquire) == 1;
-    return in ? pin + pos : pread_fetch(fd, pos, want, buf);
-  };
-  const auto seg_begin = [&](uint64_t i, uint64_t a, uint64_t b) -> int {
-    if (i >= nseg_max || i >= k || a != i * seg_len) return SF_EINVAL;  // the plan must be cut_joined's
-    if (!pread_fetch(fd, a, b - a, pin + a)) return SF_EIO;
-    if (hipSetDevice(dev) != hipSuccess ||
-        hipMemcpyAsync(dfile + a, pin + a, b - a, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
-      (void)hipGetLastError();
-      return SF_ENODEV;
-    }
-    seg_in[i].store(1, std::memory_order_release);
-    return SF_OK;
-  };
   const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
   const auto t0 = std::chrono::steady_clock::now();
   auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  double t_cut = 0, t_dev = 0;
+  std::vector<sf_block_sig> rows_v;
+  sf_host_sha1_stream bh;
+  sf_host_sha1_begin(&bh);
+  const uint64_t nseg_max = 4096;
+  std::vector<std::atomic<int>> seg_in(nseg_max);
   std::vector<uint64_t> ends;
-  rc = cut_joined(fetch, len, ops, threads, seg_begin, ends);
-  const double t_cut = ms();
-  if (rc == SF_OK && !stamp_of(fd, &after, nullptr)) rc = SF_EIO;
-  if (rc == SF_OK && !same_stamp(before, after)) rc = SF_EAGAIN;  // written while read: not one version's rows
-  if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
-  if (rc != SF_OK) return rc;
-  // 2. hash: the joined list, one launch over the file's bytes already in HBM
-  const uint64_t n = ends.size();
-  sf_block_sig* out = static_cast<sf_block_sig*>(malloc((n ? n : 1) * sizeof(sf_block_sig)));
-  if (!out) return SF_ENOMEM;
-  struct Free {
-    sf_block_sig*& p;
-    ~Free() { free(p); }
-  } guard{out};
-  uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
-  if (n) {
-    const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
-    if ((rc = res.pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
-        (rc = res.dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
-        (rc = res.pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
-        (rc = res.dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
-      return rc;
-    uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
-    uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);
-    for (uint64_t j = 0, b = 0; j < n; b = ends[j], j++) {
-      if (ends[j] - b > 0xFFFFFFFFull) return SF_EINVAL;
-      lo[j] = b;
-      lz[j] = (uint32_t)(ends[j] - b);
+  // Window by window: bytes [A, B) read once into the pinned window by the
+  // threads that cut them (a segment each, its copy to HBM started at once),
+  // cut and joined; the chunks a boundary closes inside the window are hashed
+  // from HBM, and the next window starts at the last of those boundaries (the
+  // chunk running over B is cut again from there).
+  for (uint64_t A = 0; A < len || (len == 0 && A == 0);) {
+    const uint64_t B = std::min(len, A + W);
+    const bool eof = B == len;
+    const uint64_t k = seg_count(A, B, threads);
+    if (k > nseg_max) return SF_EINVAL;
+    const uint64_t seg_len = std::max<uint64_t>(1, (B - A) / k);
+    for (uint64_t i = 0; i < k; i++) seg_in[i].store(0, std::memory_order_relaxed);
+    auto seg_of = [&](uint64_t pos) { return std::min<uint64_t>((pos - A) / seg_len, k - 1); };
+    const Fetch fetch = [&](uint64_t pos, uint64_t want, uint8_t* buf) -> const uint8_t* {
+      bool in = true;
+      for (uint64_t j = seg_of(pos); in && j <= seg_of(pos + want - 1); j++)
+        in = seg_in[j].load(std::memory_order_acquire) == 1;
+      return in ? pin + (pos - A) : pread_fetch(fd, pos, want, buf);
+    };
+    const auto seg_begin = [&](uint64_t i, uint64_t a, uint64_t b) -> int {
+      if (i >= k || a != A + i * seg_len) return SF_EINVAL;  // the plan must be cut_joined's
+      if (!pread_fetch(fd, a, b - a, pin + (a - A))) return SF_EIO;
+      if (hipSetDevice(dev) != hipSuccess ||
+          hipMemcpyAsync(dwin + (a - A), pin + (a - A), b - a, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
+        (void)hipGetLastError();
+        return SF_ENODEV;
+      }
+      seg_in[i].store(1, std::memory_order_release);
+      return SF_OK;
+    };
+    const double c0 = ms();
+    rc = len ? cut_joined(fetch, A, B, eof, ops, threads, seg_begin, ends) : SF_OK;
+    t_cut += ms() - c0;
+    if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
+    if (rc != SF_OK) return rc;
+    if (!eof && ends.empty()) {  // no boundary in a whole window (a chunk longer than W): two calls
+      SF_HIP(hipStreamSynchronize(st[0]));
+      uint64_t *o = nullptr, n = 0;
+      uint32_t* z = nullptr;
+      if ((rc = sf_cut_fd_body(fd, &before, ops, threads, &o, &z, &n)) != SF_OK) return rc;
+      sf_block_sig* out = static_cast<sf_block_sig*>(malloc((n ? n : 1) * sizeof(sf_block_sig)));
+      rc = out ? sf_index_fd_blocks(fd, &before, o, z, n, out, blocks_hash) : SF_ENOMEM;
+      free(o);
+      free(z);
+      if (rc != SF_OK) {
+        free(out);
+        return rc;
+      }
+      *rows = out;
+      *n_out = n;
+      return SF_OK;
     }
-    SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[0]));
-    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(dlist);
-    if ((rc = launch_table(dfile, len, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
-                           st[0])) != SF_OK)
-      return rc;
-    SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[0]));
-    const double t_issue = ms();
-    SF_HIP(hipStreamSynchronize(st[0]));
-    if (trace)
-      fprintf(stderr, "sf_index_fd_cut trace: %llu B, %llu blocks: cut+join %.3f, list+issue %.3f, device wait %.3f ms\n",
-              (unsigned long long)len, (unsigned long long)n, t_cut, t_issue - t_cut, ms() - t_issue);
-    for (uint64_t j = 0; j < n; j++) {
-      out[j].offset = lo[j];
-      out[j].size = lz[j];
-      memcpy(out[j].sha1, pdig + 20 * j, 20);
+    // hash the window's chunks: one launch over its bytes already in HBM
+    const uint64_t n = ends.size();
+    const double d0 = ms();
+    if (n) {
+      uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
+      const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
+      if ((rc = res.pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
+          (rc = res.dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
+          (rc = res.pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
+          (rc = res.dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
+        return rc;
+      uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
+      uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);
+      for (uint64_t j = 0, b = A; j < n; b = ends[j], j++) {
+        if (ends[j] - b > 0xFFFFFFFFull) return SF_EINVAL;
+        lo[j] = b - A;  // offsets in the window
+        lz[j] = (uint32_t)(ends[j] - b);
+      }
+      SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[0]));
+      const uint64_t* d_off = reinterpret_cast<const uint64_t*>(dlist);
+      if ((rc = launch_table(dwin, B - A, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
+                             st[0])) != SF_OK)
+        return rc;
+      SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[0]));
+      SF_HIP(hipStreamSynchronize(st[0]));  // also: the window's copies are done before it is refilled
+      const size_t r0 = rows_v.size();
+      rows_v.resize(r0 + n);
+      for (uint64_t j = 0; j < n; j++) {
+        rows_v[r0 + j].offset = A + lo[j];
+        rows_v[r0 + j].size = lz[j];
+        memcpy(rows_v[r0 + j].sha1, pdig + 20 * j, 20);
+      }
+      sf_host_sha1_update(&bh, pdig, n * 20);  // compute_blocks_hash (src/index.rs:661-682), in order
+    } else {
+      SF_HIP(hipStreamSynchronize(st[0]));
     }
-  } else {
-    SF_HIP(hipStreamSynchronize(st[0]));
+    t_dev += ms() - d0;
+    if (eof) break;
+    A = ends.back();
   }
-  static const uint8_t kNone[1] = {0};
-  sf_host_sha1_impl(n ? pdig : kNone, n * 20, blocks_hash, 0);  // compute_blocks_hash (src/index.rs:661-682)
+  if (!stamp_of(fd, &after, nullptr)) return SF_EIO;
+  if (!same_stamp(before, after)) return SF_EAGAIN;  // written while read: not one version's rows
+  if (trace)
+    fprintf(stderr, "sf_index_fd_cut trace: %llu B, %zu blocks: cut+join %.3f, device %.3f, total %.3f ms\n",
+            (unsigned long long)len, rows_v.size(), t_cut, t_dev, ms());
+  sf_block_sig* out = static_cast<sf_block_sig*>(malloc((rows_v.empty() ? 1 : rows_v.size()) * sizeof(sf_block_sig)));
+  if (!out) return SF_ENOMEM;
+  if (!rows_v.empty()) memcpy(out, rows_v.data(), rows_v.size() * sizeof(sf_block_sig));
+  sf_host_sha1_final(&bh, blocks_hash);
   *rows = out;
-  *n_out = n;
-  guard.p = nullptr;
+  *n_out = rows_v.size();
   return SF_OK;
 }
 

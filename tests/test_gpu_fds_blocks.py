@@ -421,3 +421,28 @@ def test_index_native_chunker_on_the_gpu(gpu, tmp_path, batch):
             assert bh.to_sql() == oracle.blocks_hash(dig).hex(), name
     finally:
         lib.sf_zpaq_standin_ops_free(ops)
+
+
+@pytest.mark.parametrize("window_mib,n", [(1, 5 << 20), (8, (20 << 20) + 12345), (16, (37 << 20) + 1)])
+def test_index_fd_cut_small_windows(gpu, tmp_path, knobs, window_mib, n):
+    """sf_index_fd_cut by windows (SF_TEST_CUT_WINDOW_MIB here, 512 MiB by
+    default; 8 and 16 MiB windows hold 2 and 4 segments): every window ends at
+    the last boundary inside it and the next starts there, so the chunk across
+    each seam is cut again; rows and blocks_hash still equal the one-stream
+    cut hashed by the oracle."""
+    knobs.set("SF_TEST_CUT_WINDOW_MIB", window_mib)
+    lib, ops = _standin_ops()
+    try:
+        data = oracle.splitmix_bytes(n, 7750)
+        p = tmp_path / "w"
+        data.tofile(p)
+        sizes = oracle.zpaq_standin_sizes(data).astype(np.uint32)
+        offs = _offs(sizes)
+        dig = oracle.index_blocks(data, offs, sizes)
+        for threads in (1, 4, 16):
+            with open(p, "rb") as f:
+                rows, bh = host.index_fd_cut(f.fileno(), ops, threads)
+            assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes), threads
+            assert np.array_equal(rows["sha1"], dig) and bh == oracle.blocks_hash(dig), threads
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)
