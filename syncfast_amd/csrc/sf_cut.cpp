@@ -111,12 +111,14 @@ inline uint64_t seg_count(uint64_t A, uint64_t B, uint32_t threads) {
 
 // The segments of bytes [A, B) and the join (the file comment); A is a true
 // boundary, and B the end of the file if eof.  `fetch` supplies the bytes,
-// `seg_begin(i, a, b)` runs on the thread that takes segment i = [a, b)
-// before it is cut (the fused route reads the segment and starts its copy
-// there).  The true chain's ends in (A, B] go to `ends`; without eof, only
+// `seg_begin(i, a, b)` / `seg_end` run on the thread that takes segment i =
+// [a, b) before and after it is cut (the fused route claims the segment, then
+// starts its copy to HBM once every byte of it has been read).  The true chain's ends in (A, B] go to `ends`; without eof, only
 // the ends of chunks that a boundary closes inside [A, B).
+using SegHook = std::function<int(uint64_t, uint64_t, uint64_t)>;
+
 int cut_joined(const Fetch& fetch, uint64_t A, uint64_t B, bool eof, const sf_chunker_ops* ops, uint32_t threads,
-               const std::function<int(uint64_t, uint64_t, uint64_t)>& seg_begin, std::vector<uint64_t>& ends) {
+               const SegHook& seg_begin, std::vector<uint64_t>& ends, const SegHook& seg_end = nullptr) {
   ends.clear();
   if (B <= A) return SF_OK;
   const uint64_t len = B;
@@ -139,6 +141,7 @@ int cut_joined(const Fetch& fetch, uint64_t A, uint64_t B, bool eof, const sf_ch
         out.push_back(e);
         return e < stop;
       });
+      if (rcs[i] == SF_OK && seg_end) rcs[i] = seg_end(i, P[i], P[i + 1]);
     }
   });
   for (int rc : rcs)
@@ -281,6 +284,8 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   sf_host_sha1_begin(&bh);
   const uint64_t nseg_max = 4096;
   std::vector<std::atomic<int>> seg_in(nseg_max);
+  std::vector<std::atomic<const void*>> seg_owner(nseg_max);  // the thread cutting segment i (its tl_me)
+  for (auto& o : seg_owner) o.store(nullptr, std::memory_order_relaxed);
   std::vector<uint64_t> ends;
   // Window by window: bytes [A, B) read once into the pinned window by the
   // threads that cut them (a segment each, its copy to HBM started at once),
@@ -295,25 +300,42 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     const uint64_t seg_len = std::max<uint64_t>(1, (B - A) / k);
     for (uint64_t i = 0; i < k; i++) seg_in[i].store(0, std::memory_order_relaxed);
     auto seg_of = [&](uint64_t pos) { return std::min<uint64_t>((pos - A) / seg_len, k - 1); };
+    auto seg_hi = [&](uint64_t j) { return j + 1 == k ? B : A + (j + 1) * seg_len; };
+    // A thread reads the segment it cuts piece by piece into its place in the
+    // pinned window and cuts each piece while it is in cache; bytes of a
+    // segment another thread owns come from pread into a private buffer until
+    // that segment is complete, then from the window.
+    static thread_local char tl_me;
     const Fetch fetch = [&](uint64_t pos, uint64_t want, uint8_t* buf) -> const uint8_t* {
+      const uint64_t j = seg_of(pos);
       bool in = true;
-      for (uint64_t j = seg_of(pos); in && j <= seg_of(pos + want - 1); j++)
-        in = seg_in[j].load(std::memory_order_acquire) == 1;
-      return in ? pin + (pos - A) : pread_fetch(fd, pos, want, buf);
+      for (uint64_t q = j; in && q <= seg_of(pos + want - 1); q++)
+        in = seg_in[q].load(std::memory_order_acquire) == 1;
+      if (in) return pin + (pos - A);
+      if (seg_owner[j].load(std::memory_order_relaxed) != &tl_me) return pread_fetch(fd, pos, want, buf);
+      const uint64_t own = std::min(want, seg_hi(j) - pos);  // this thread's segment: into the window
+      if (own == want) return pread_fetch(fd, pos, want, pin + (pos - A));
+      const uint8_t* p = pread_fetch(fd, pos, want, buf);  // a piece across the segment's end
+      if (p) memcpy(pin + (pos - A), p, own);
+      return p;
     };
     const auto seg_begin = [&](uint64_t i, uint64_t a, uint64_t b) -> int {
-      if (i >= k || a != A + i * seg_len) return SF_EINVAL;  // the plan must be cut_joined's
-      if (!pread_fetch(fd, a, b - a, pin + (a - A))) return SF_EIO;
+      if (i >= k || a != A + i * seg_len || b != seg_hi(i)) return SF_EINVAL;  // the plan must be cut_joined's
+      seg_owner[i].store(&tl_me, std::memory_order_relaxed);
+      return SF_OK;
+    };
+    const auto seg_end = [&](uint64_t i, uint64_t a, uint64_t b) -> int {  // every byte of [a, b) is in
       if (hipSetDevice(dev) != hipSuccess ||
           hipMemcpyAsync(dwin + (a - A), pin + (a - A), b - a, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
         (void)hipGetLastError();
         return SF_ENODEV;
       }
+      seg_owner[i].store(nullptr, std::memory_order_relaxed);
       seg_in[i].store(1, std::memory_order_release);
       return SF_OK;
     };
     const double c0 = ms();
-    rc = len ? cut_joined(fetch, A, B, eof, ops, threads, seg_begin, ends) : SF_OK;
+    rc = len ? cut_joined(fetch, A, B, eof, ops, threads, seg_begin, ends, seg_end) : SF_OK;
     t_cut += ms() - c0;
     if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
     if (rc != SF_OK) return rc;
