@@ -285,6 +285,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   const uint64_t nseg_max = 4096;
   std::vector<std::atomic<int>> seg_in(nseg_max);
   std::vector<std::atomic<const void*>> seg_owner(nseg_max);  // the thread cutting segment i (its tl_me)
+  std::atomic<bool> copy_failed{false};
   for (auto& o : seg_owner) o.store(nullptr, std::memory_order_relaxed);
   std::vector<uint64_t> ends;
   // Window by window: bytes [A, B) read once into the pinned window by the
@@ -302,9 +303,9 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     auto seg_of = [&](uint64_t pos) { return std::min<uint64_t>((pos - A) / seg_len, k - 1); };
     auto seg_hi = [&](uint64_t j) { return j + 1 == k ? B : A + (j + 1) * seg_len; };
     // A thread reads the segment it cuts piece by piece into its place in the
-    // pinned window and cuts each piece while it is in cache; bytes of a
-    // segment another thread owns come from pread into a private buffer until
-    // that segment is complete, then from the window.
+    // pinned window, starts the piece's copy to HBM and cuts it while it is in
+    // cache; bytes of a segment another thread owns come from pread into a
+    // private buffer until that segment is complete, then from the window.
     static thread_local char tl_me;
     const Fetch fetch = [&](uint64_t pos, uint64_t want, uint8_t* buf) -> const uint8_t* {
       const uint64_t j = seg_of(pos);
@@ -314,28 +315,35 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
       if (in) return pin + (pos - A);
       if (seg_owner[j].load(std::memory_order_relaxed) != &tl_me) return pread_fetch(fd, pos, want, buf);
       const uint64_t own = std::min(want, seg_hi(j) - pos);  // this thread's segment: into the window
-      if (own == want) return pread_fetch(fd, pos, want, pin + (pos - A));
-      const uint8_t* p = pread_fetch(fd, pos, want, buf);  // a piece across the segment's end
-      if (p) memcpy(pin + (pos - A), p, own);
+      const uint8_t* p = own == want ? pread_fetch(fd, pos, want, pin + (pos - A))
+                                     : pread_fetch(fd, pos, want, buf);  // a piece across the segment's end
+      if (!p) return nullptr;
+      if (own != want) memcpy(pin + (pos - A), p, own);
+      // the piece's copy to HBM starts now, while the chunker cuts it
+      if (hipMemcpyAsync(dwin + (pos - A), pin + (pos - A), own, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
+        (void)hipGetLastError();
+        copy_failed.store(true, std::memory_order_relaxed);
+        return nullptr;
+      }
       return p;
     };
     const auto seg_begin = [&](uint64_t i, uint64_t a, uint64_t b) -> int {
       if (i >= k || a != A + i * seg_len || b != seg_hi(i)) return SF_EINVAL;  // the plan must be cut_joined's
-      seg_owner[i].store(&tl_me, std::memory_order_relaxed);
-      return SF_OK;
-    };
-    const auto seg_end = [&](uint64_t i, uint64_t a, uint64_t b) -> int {  // every byte of [a, b) is in
-      if (hipSetDevice(dev) != hipSuccess ||
-          hipMemcpyAsync(dwin + (a - A), pin + (a - A), b - a, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
+      if (hipSetDevice(dev) != hipSuccess) {  // this thread enqueues the segment's copies
         (void)hipGetLastError();
         return SF_ENODEV;
       }
+      seg_owner[i].store(&tl_me, std::memory_order_relaxed);
+      return SF_OK;
+    };
+    const auto seg_end = [&](uint64_t i, uint64_t, uint64_t) -> int {  // every byte of segment i is in
       seg_owner[i].store(nullptr, std::memory_order_relaxed);
       seg_in[i].store(1, std::memory_order_release);
       return SF_OK;
     };
     const double c0 = ms();
     rc = len ? cut_joined(fetch, A, B, eof, ops, threads, seg_begin, ends, seg_end) : SF_OK;
+    if (copy_failed.load(std::memory_order_relaxed)) rc = SF_ENODEV;
     t_cut += ms() - c0;
     if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
     if (rc != SF_OK) return rc;
