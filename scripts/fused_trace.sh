@@ -1,3 +1,6 @@
+#!/bin/bash
+# sf_index_fd_cut's phase times (SF_TRACE=1) on configs[0]'s 64 MiB file, four
+# passes in one process, then the two-call route (-W) for comparison.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/ftrace
 python3 -c "
