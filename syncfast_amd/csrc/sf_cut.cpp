@@ -21,9 +21,12 @@
 // matched, so the result is the sequential one for any thread count; the
 // parallel part only saves time when the chains meet early, which for a
 // chunker whose state is a hash of recent bytes happens within a few chunks.
-// sf_index_fd_cut adds the hashing: every segment is read once into a pinned
-// copy of the file, copied to HBM while it is being cut, and the joined list
-// is hashed from there (sha1_table_kernel) -- no second read of the file.
+// sf_index_fd_cut adds the hashing, window by window (up to 512 MiB): each
+// thread reads its segment piece by piece into a pinned copy of the window,
+// starts each piece's copy to HBM and cuts it while it is in cache; the
+// joined list is hashed from HBM (sha1_table_kernel) -- no second read of the
+// file.  A window keeps the chunks a boundary closes inside it, and the next
+// window starts at the last such boundary.
 #include <errno.h>
 #include <stdint.h>
 #include <stdlib.h>
