@@ -31,7 +31,10 @@
  *     sf_index_fds_blocks call while the threads cut the next batch; -q
  *     prints only the first and last file's rows (every file's blocks_hash);
  *     -P n: the whole run n times in one process (the first pays the
- *     library's stage allocations), a timing line per pass.
+ *     library's stage allocations), a timing line per pass; -K MiB: a file
+ *     of at least this size (default 64, configs[0]'s file; 0 = never) is
+ *     indexed alone in its place through sf_index_fd_cut on the -j threads
+ *     (cut in parallel, read once) instead of being cut on one thread.
  * Regular files (default mode) go through the same one-open form:
  * sf_file_stamp_fd + sf_index_fd_fixed on the open descriptor.
  */
@@ -472,7 +475,7 @@ static int zpaq_cut_fd(int fd, uint8_t *buf, size_t bufsz, uint64_t **offs_io, u
  * -T: one JSON line on stderr with the wall time and its parts. */
 typedef struct {
     const char *path;
-    int fd, rc;
+    int fd, rc, large; /* large: opened and stamped only, cut + hashed by sf_index_fd_cut */
     sf_file_stamp st;
     uint64_t *offs, cap, n, bytes;
     uint32_t *sizes;
@@ -506,8 +509,9 @@ static void *cut_worker(void *arg) {
         j->rc = j->fd < 0 ? SF_EIO : !buf ? SF_ENOMEM : sf_file_stamp_fd(j->fd, &j->st);
         const double t1 = now_s();
         double rd = 0;
-        if (j->rc == SF_OK) j->rc = zpaq_cut_fd(j->fd, buf, kRead, &j->offs, &j->sizes, &j->cap, &j->n, &j->bytes, &rd);
-        if (j->rc == SF_OK && j->bytes != j->st.size) j->rc = SF_EAGAIN;  /* written while cut */
+        if (j->rc == SF_OK && !j->large)
+            j->rc = zpaq_cut_fd(j->fd, buf, kRead, &j->offs, &j->sizes, &j->cap, &j->n, &j->bytes, &rd);
+        if (j->rc == SF_OK && !j->large && j->bytes != j->st.size) j->rc = SF_EAGAIN;  /* written while cut */
         const double dt = now_s() - t0;
         pthread_mutex_lock(&P->mu);
         P->chunk_s += dt;
@@ -537,8 +541,40 @@ static void *stat_worker(void *arg) { /* the sizes for the batch plan, 64 files 
     return NULL;
 }
 
+/* A large file of -Z -M, alone in its batch: cut on `threads` threads and
+ * hashed from one read of the walk's open descriptor (sf_index_fd_cut), with
+ * the stamp taken at that open; SF_EAGAIN (written meanwhile): again, alone,
+ * from a new open (index_zpaq_fused's retries). */
+static int index_zpaq_large(cut_job *j, int threads, int quiet, int edge, uint64_t *blocks, double *hash_s) {
+    const sf_chunker_ops ops = {zpaq_create, zpaq_next, zpaq_destroy, NULL};
+    sf_block_sig *rows = NULL;
+    uint64_t n = 0;
+    uint8_t bh[20];
+    const double t0 = now_s();
+    int rc = sf_index_fd_cut(j->fd, &j->st, &ops, (uint32_t)threads, &rows, &n, bh);
+    *hash_s += now_s() - t0;
+    if (rc == SF_EAGAIN) {
+        close(j->fd);
+        j->fd = -1;
+        return index_zpaq_fused(j->path, (uint32_t)threads, 0);
+    }
+    if (rc == SF_OK) {
+        j->bytes = j->st.size;
+        *blocks += n;
+        if (quiet == 2) { /* an untimed warm-up pass: no output */
+        } else if (!quiet || edge) print_rows(j->path, rows, n, bh);
+        else {
+            char h[41];
+            hex(bh, h);
+            printf("file %s blocks %llu\nblocks_hash %s\n", j->path, (unsigned long long)n, h);
+        }
+    }
+    sf_free_rows(rows);
+    return rc;
+}
+
 static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_bytes, uint64_t stage_bytes, int timing,
-                           int quiet) {
+                           int quiet, uint64_t large_bytes) {
     cut_job *jobs = calloc((size_t)(n ? n : 1), sizeof(cut_job));
     int *batch_of = malloc((size_t)(n ? n : 1) * sizeof(int)), nb = 0;
     int *batch_left = calloc((size_t)(n ? n : 1), sizeof(int)), *batch_first = calloc((size_t)n + 2, sizeof(int));
@@ -564,10 +600,12 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         stat_worker(&S);
         for (int t = 0; t < ns; t++) pthread_join(st[t], NULL);
     }
-    for (int k = 0; k < n; k++) { /* batches by size and descriptor count */
+    for (int k = 0; k < n; k++) { /* batches by size and descriptor count; a large file alone */
         jobs[k].path = paths[k];
         jobs[k].fd = -1;
-        if (k == 0 || acc >= batch_bytes || k - batch_first[nb - 1] >= max_files) {
+        jobs[k].large = large_bytes && fsize[k] >= large_bytes;
+        if (k == 0 || acc >= batch_bytes || k - batch_first[nb - 1] >= max_files || jobs[k].large ||
+            jobs[k - 1].large) {
             batch_first[nb++] = k;
             acc = 0;
         }
@@ -592,6 +630,24 @@ static int index_zpaq_many(char **paths, int n, int threads, uint64_t batch_byte
         while (batch_left[b] > 0) pthread_cond_wait(&P.cv, &P.mu);
         pthread_mutex_unlock(&P.mu);
         t_wait += now_s() - tw;
+        if (m == 1 && jobs[f0].large) { /* the large file, in its place */
+            cut_job *j = &jobs[f0];
+            rc = j->rc != SF_OK ? j->rc : index_zpaq_large(j, threads, quiet, f0 == 0 || f0 == n - 1, &total_blocks,
+                                                                  &t_hash);
+            if (rc == SF_EAGAIN) { /* written between its open and its stamp check: once more, alone */
+                if (j->fd >= 0) close(j->fd);
+                j->fd = -1;
+                rc = index_zpaq_fused(j->path, (uint32_t)threads, 0);
+            }
+            if (j->fd >= 0) close(j->fd);
+            j->fd = -1;
+            total_bytes += rc == SF_OK ? j->bytes : 0;
+            pthread_mutex_lock(&P.mu);
+            P.hashed = b;
+            pthread_cond_broadcast(&P.cv);
+            pthread_mutex_unlock(&P.mu);
+            continue;
+        }
         int *fds = malloc((size_t)m * sizeof(int)), *fst = malloc((size_t)m * sizeof(int));
         sf_file_stamp *sts = malloc((size_t)m * sizeof(sf_file_stamp));
         const uint64_t **po = malloc((size_t)m * sizeof(void *));
@@ -813,7 +869,7 @@ int main(int argc, char **argv) {
     uint32_t bs = 4096;
     int many = 0, buffer = 0, shards = 0, lookup = 0, cdc = 0, zpaq = 0, timing = 0, threads = 1, quiet = 0;
     int passes = 1, multi = -1, cut_threads = -1, two_calls = 0;
-    uint64_t batch_mib = 256, stage_mib = 0;
+    uint64_t batch_mib = 256, stage_mib = 0, large_mib = 64;
     long long wire = -1, wire_cdc = -1;
     int i = 1;
     for (; i < argc; i++) {
@@ -827,6 +883,7 @@ int main(int argc, char **argv) {
         else if (strcmp(argv[i], "-W") == 0) two_calls = 1;
         else if (i + 1 < argc && strcmp(argv[i], "-S") == 0) batch_mib = strtoull(argv[++i], NULL, 10);
         else if (i + 1 < argc && strcmp(argv[i], "-G") == 0) stage_mib = strtoull(argv[++i], NULL, 10);
+        else if (i + 1 < argc && strcmp(argv[i], "-K") == 0) large_mib = strtoull(argv[++i], NULL, 10);
         else if (strcmp(argv[i], "-M") == 0) many = 2;
         else if (strcmp(argv[i], "-q") == 0) quiet = 1;
         else if (i + 1 < argc && strcmp(argv[i], "-P") == 0) passes = atoi(argv[++i]);
@@ -839,7 +896,7 @@ int main(int argc, char **argv) {
         else break;
     }
     if (i >= argc && wire < 0 && wire_cdc < 0) {
-        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-p cut_threads [-W]] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-q] [-P passes]] | -s shards | -X devices] "
+        fprintf(stderr, "usage: %s [-b block_size] [-m | -B | -C | -Z [-T] [-p cut_threads [-W]] [-M [-j threads] [-S batch_mib] [-G stage_mib] [-K large_mib] [-q] [-P passes]] | -s shards | -X devices] "
                         "path... | -w bytes | -v bytes | -L dst src\n",
                 argv[0]);
         return 2;
@@ -875,7 +932,7 @@ int main(int argc, char **argv) {
         int rc = SF_OK;
         for (int pass = 0; pass < passes && rc == SF_OK; pass++)
             rc = index_zpaq_many(argv + i, argc - i, threads > 0 ? threads : 1, batch_mib << 20, stage_mib << 20, timing,
-                                 pass + 1 < passes ? 2 : quiet);
+                                 pass + 1 < passes ? 2 : quiet, large_mib << 20);
         if (rc != SF_OK) fprintf(stderr, "zpaq many: %s\n", sf_strerror(rc));
         sf_release_host_cache();
         return rc != SF_OK;

@@ -425,7 +425,8 @@ typedef struct sf_chunker_ops {
  * not used), cut by `ops`, exactly as one chunker streaming the file from its
  * first byte would cut it (the loop of src/index.rs:629-647 without the
  * SHA-1).  With threads > 1 (0 = the library's reader count) the file is
- * split into up to `threads` segments of at least 1 MiB; a chunker starts
+ * split into up to `threads` segments of at least 4 MiB (a file under 8 MiB is
+ * cut on one thread); a chunker starts
  * fresh at each segment's first byte and cuts speculatively; the segments are
  * then joined left to right: from the last boundary known to be right, the
  * file is cut again on one thread only until a boundary coincides with one of
@@ -496,6 +497,20 @@ int sf_index_file_multi(const char *path, uint32_t block_size, uint32_t n_device
  * loaded or a communicator not made. */
 int sf_index_device_multi(uint32_t n_devices, const void *const *d_shards, uint64_t file_len, uint32_t block_size,
                           void *const *d_digests, uint32_t root, void *d_table, void *const *streams);
+
+/* sf_index_device_multi with the exchange on streams of its own: shard r is
+ * hashed on hash_streams[r] (NULL: each device's null stream) and sent -- and,
+ * on the root, received -- on gather_streams[r], which first waits for device
+ * r's hashing (an event the library records on hash_streams[r]; NULL
+ * gather_streams: the hash streams, i.e. sf_index_device_multi).  A caller
+ * indexing file after file (each file's table gathered to its owner, config
+ * 4 of BASELINE.json over and over) can then hash file i+1 while file i's
+ * tables are in flight: d_digests[r] may be written again, and d_table read,
+ * once gather_streams[r] / gather_streams[root] have run past the call.
+ * Errors as sf_index_device_multi. */
+int sf_index_device_multi_ex(uint32_t n_devices, const void *const *d_shards, uint64_t file_len,
+                             uint32_t block_size, void *const *d_digests, uint32_t root, void *d_table,
+                             void *const *hash_streams, void *const *gather_streams);
 
 /* compute_blocks_hash (src/index.rs:661-682) on the host: SHA-1 over the
  * n 20-byte digests in order.  Sequential by definition; runs on a host

@@ -51,6 +51,28 @@ int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uint32_t mbits
 typedef void (*sf_test_read_hook_fn)(void* arg, uint64_t window);
 int sf_test_set_read_hook(sf_test_read_hook_fn fn, void* arg);
 
+/* The gather plan of sf_index_device_multi / _ex for n_devices shards of a
+ * file_len-byte file at block_size, gathered to `root` (self_gather: the
+ * one-device self send/recv of SF_TEST_MULTI_SELF_GATHER, n_devices == 1
+ * only).  Per device r (n_devices entries each): table_offset[r] = where its
+ * rows start in d_table (bytes), bytes[r] = its digest bytes, route[r] = 0
+ * (empty shard: nothing hashed or sent), 1 (the root's rows, hashed in place
+ * into d_table) or 2 (hashed into d_digests[r] and sent to the root, which
+ * receives them at table_offset[r]).  Host only. */
+int sf_test_multi_plan(uint64_t file_len, uint32_t block_size, uint32_t n_devices, uint32_t root, int self_gather,
+                       uint64_t *table_offset, uint64_t *bytes, int *route);
+
+/* Cross-XCD counter litmus (sf_litmus.hip): does a read of a counter see
+ * adds made on other XCDs after the reading XCD's L2 holds its line?
+ * mode 0 reads with a relaxed agent-scope atomic load, mode 1 with an
+ * agent-scope atomic add of an opaque zero (the fused launch's poll,
+ * sf_kernels.hpp coherent_read_u32).  One launch on the current device,
+ * synchronous.  out[8]: status (0 ok, 1 a hand-shake wait ran out), the
+ * reader's XCD id, adds made from other XCDs, first read, read after every
+ * add returned, a read-modify-write read after that, mode, 0.  A stale form
+ * gives out[4] == out[3] < out[2] == out[5]. */
+int sf_test_xcd_litmus(int mode, uint32_t out[8]);
+
 #ifdef __cplusplus
 }
 #endif

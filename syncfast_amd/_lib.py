@@ -35,7 +35,7 @@ EXPORTED = (
     "sf_index_device_batch_chained_cols",
     "sf_fill_splitmix_device", "sf_wire_file_blocks_device", "sf_wire_blocks_device", "sf_wire_blocks_fd", "sf_wire_file_blocks_fd", "sf_index_buffer", "sf_index_buffer_blocks", "sf_index_file_blocks", "sf_file_stamp_fd", "sf_index_fd_blocks", "sf_index_fd_fixed", "sf_index_file", "sf_index_file_range", "sf_index_fd", "sf_free_rows", "sf_index_files",
     "sf_index_fds_blocks", "sf_cut_fd", "sf_free_cuts", "sf_index_fd_cut", "sf_shard_range", "sf_index_file_multi",
-    "sf_index_device_multi",
+    "sf_index_device_multi", "sf_index_device_multi_ex",
     "sf_blocks_hash", "sf_blocks_hash_sigs", "sf_sha1_host",
     "sf_block_set_build", "sf_block_set_lookup", "sf_block_set_free",
 )
@@ -43,7 +43,7 @@ EXPORTED = (
 # the explicit-list processing order.
 EXPORTED_TEST = ("sf_test_set_knob", "sf_test_get_knob", "sf_test_get_stat", "sf_test_table_order",
                  "sf_test_table_order_bits",
-                 "sf_test_set_read_hook")
+                 "sf_test_set_read_hook", "sf_test_xcd_litmus", "sf_test_multi_plan")
 
 
 class SfError(OSError):
@@ -136,6 +136,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_shard_range.argtypes = [u64, u32, u32, u32, pu64, pu64]
     L.sf_index_file_multi.argtypes = [ctypes.c_char_p, u32, u32, ctypes.POINTER(BlockSig), u64, pu64, vp]
     L.sf_index_device_multi.argtypes = [u32, vp, u64, u32, vp, u32, vp, vp]
+    L.sf_index_device_multi_ex.argtypes = [u32, vp, u64, u32, vp, u32, vp, vp, vp]
     L.sf_blocks_hash.argtypes = [vp, u64, vp]
     L.sf_blocks_hash_sigs.argtypes = [ctypes.POINTER(BlockSig), u64, vp]
     L.sf_sha1_host.argtypes = [vp, u64, vp]
@@ -149,6 +150,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.sf_test_table_order.argtypes = [vp, u64, vp, vp]
     L.sf_test_table_order_bits.argtypes = [vp, u64, ctypes.c_uint32, vp, vp]
     L.sf_test_set_read_hook.argtypes = [READ_HOOK, vp]
+    L.sf_test_xcd_litmus.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+    L.sf_test_multi_plan.argtypes = [u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp, vp, vp]
     for name in EXPORTED + EXPORTED_TEST:
         if name not in ("sf_version", "sf_strerror", "sf_free_rows"):
             getattr(L, name).restype = ctypes.c_int

@@ -199,11 +199,19 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
 // path, which never waits.  (b): d_status (device int32) receives
 // SF_ETIMEDOUT; with d_status == NULL the unstaged path is taken.
 // SF_TEST_CHAIN_SPIN_LIMIT (test hook) bounds the polls of each wait
-// (default 2^24, several seconds).
+// (default 2^24, several seconds): a backstop, since the poll is a coherent
+// read (sf_kernels.hpp, coherent_read_u32).
 
 inline uint32_t chain_spin_limit() {
   const int64_t v = knob(K_TEST_CHAIN_SPIN_LIMIT);
   return v >= 0 ? (uint32_t)std::min<int64_t>(v, 0xFFFFFFFFll) : (1u << 24);
+}
+// SF_TEST_CHAIN_POLL_GAP_US (test hook): a chain lane whose poll did not match
+// waits this long (100 MHz wall-clock ticks) before the next, so a test can
+// put a lane's first poll before the block waves finish and its next after.
+inline uint32_t chain_poll_gap() {
+  const int64_t v = knob(K_TEST_CHAIN_POLL_GAP_US);
+  return v > 0 ? (uint32_t)std::min<int64_t>(v * 100, 0xFFFFFFFFll) : 0u;
 }
 
 int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
@@ -249,7 +257,7 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
   sfi::clear_stale_error();
   hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
                      nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, d_status,
-                     chain_spin_limit());
+                     chain_spin_limit(), chain_poll_gap());
   int rc = hip_err(hipGetLastError());
   (void)hipFreeAsync(words, s);
   return rc;

@@ -40,6 +40,7 @@
 #include <atomic>
 #include <chrono>
 #include <functional>
+#include <memory>
 #include <vector>
 
 #include "host_sha1.h"
@@ -270,13 +271,16 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   SF_HIP(hipGetDevice(&dev));
   const int64_t wk = knob(K_TEST_CUT_WINDOW_MIB);  // test hook: small windows exercise the window seams
   const uint64_t W = wk > 0 ? (uint64_t)wk << 20 : kFusedMax;
-  HostLease res;
+  // held by pointer: released before the two-call fallback below, which
+  // takes a lease of its own (a nested lease would try_lock the device's
+  // cache mutex this thread already owns)
+  auto res = std::make_unique<HostLease>();
   hipStream_t* st;
   hipEvent_t* done_ev;
   uint8_t *pin = nullptr, *dwin = nullptr;
-  int rc = res.streams(st, done_ev);
-  if (rc == SF_OK) rc = res.pin(0, std::min(len, W), reinterpret_cast<void**>(&pin));
-  if (rc == SF_OK) rc = res.dev(0, std::min(len, W), reinterpret_cast<void**>(&dwin));
+  int rc = res->streams(st, done_ev);
+  if (rc == SF_OK) rc = res->pin(0, std::min(len, W), reinterpret_cast<void**>(&pin));
+  if (rc == SF_OK) rc = res->dev(0, std::min(len, W), reinterpret_cast<void**>(&dwin));
   if (rc != SF_OK) return rc;
   const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
   const auto t0 = std::chrono::steady_clock::now();
@@ -352,6 +356,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     if (rc != SF_OK) return rc;
     if (!eof && ends.empty()) {  // no boundary in a whole window (a chunk longer than W): two calls
       SF_HIP(hipStreamSynchronize(st[0]));
+      res.reset();  // the window's buffers and streams go back before sf_index_fd_blocks leases them
       uint64_t *o = nullptr, n = 0;
       uint32_t* z = nullptr;
       if ((rc = sf_cut_fd_body(fd, &before, ops, threads, &o, &z, &n)) != SF_OK) return rc;
@@ -373,10 +378,10 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     if (n) {
       uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
       const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
-      if ((rc = res.pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
-          (rc = res.dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
-          (rc = res.pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
-          (rc = res.dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
+      if ((rc = res->pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
+          (rc = res->dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
+          (rc = res->pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
+          (rc = res->dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
         return rc;
       uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
       uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);

@@ -393,21 +393,45 @@ __device__ __forceinline__ void sha1_stream_range(Sha1& st, const uint4* __restr
   }
 }
 
+// Coherent read of a counter that waves on every XCD add to: an agent-scope
+// atomic add of a zero the compiler cannot see (hipcc folds an add of a
+// literal 0 into a plain load).  A relaxed agent-scope atomic LOAD is a
+// `global_load ... sc1`: it skips the CU's L1 but is served by the reading
+// XCD's L2, which no other XCD's add invalidates -- once the line is there,
+// the reader sees a frozen count until its own XCD adds again or the line is
+// evicted (tests/test_gpu_robustness.py's XCD litmus shows
+// it).  The read-modify-write is performed where every XCD's adds are.
+__device__ __forceinline__ uint32_t coherent_read_u32(uint32_t* p) {
+  uint32_t zero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+  return __hip_atomic_fetch_add(p, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Busy-wait about `ticks` of the 100 MHz wall clock (test hook: the delay
+// between a chain lane's polls, SF_TEST_CHAIN_POLL_GAP_US).
+__device__ __forceinline__ void wait_ticks(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // One lane per file: the file's blocks_hash (src/index.rs:661-682) = SHA-1
 // over its run of run_len digest bytes, consumed in S slices of mb bytes (a
 // multiple of 64).  With stage_done, slice k is read only after
-// stage_done[k] == waves_per_stage: ONE lane polls ONE word (relaxed, agent
-// scope, s_sleep, at most spin_limit + 1 polls), then an agent-scope acquire
-// (MI355X guide, Guideline 16).  A poll that gives up stores an all-zero hash
-// and sets *status = SF_ETIMEDOUT, which the host reads back and returns (the
-// reference never yields a hash it did not compute, src/index.rs:661-682).
-// Never expected: the producers never wait, and the host keeps the chain
-// workgroups below the resident capacity (batch_staged).
+// stage_done[k] == waves_per_stage: ONE lane polls ONE word with a coherent
+// read (coherent_read_u32, s_sleep between polls, at most spin_limit + 1
+// polls), then an agent-scope acquire (MI355X guide, Guideline 16).  A poll
+// that gives up stores an all-zero hash and sets *status = SF_ETIMEDOUT,
+// which the host reads back and returns (the reference never yields a hash it
+// did not compute, src/index.rs:661-682).  Not expected: the producers never
+// wait, the host keeps the chain workgroups below the resident capacity
+// (batch_staged), and the poll sees every XCD's adds; the bound is a backstop.
+// poll_gap (test hook, wall-clock ticks): the wait after a poll that did not
+// match, instead of s_sleep(8).
 __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t f,
                                            bool valid, uint32_t run_len, uint32_t S, uint32_t mb,
-                                           const uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
+                                           uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
                                            uint8_t* __restrict__ out, int* __restrict__ status,
-                                           uint32_t spin_limit) {
+                                           uint32_t spin_limit, uint32_t poll_gap) {
   const int lane = lane_id();
   Sha1 st;
   st.init();
@@ -419,9 +443,10 @@ __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uin
       uint32_t seen = 0;
       if (lane == 0) {
         for (uint32_t spins = 0;; ++spins) {
-          seen = __hip_atomic_load(stage_done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          seen = coherent_read_u32(stage_done + k);
           if (seen >= waves_per_stage || spins >= spin_limit) break;
-          __builtin_amdgcn_s_sleep(8);
+          if (poll_gap) wait_ticks(poll_gap);
+          else __builtin_amdgcn_s_sleep(8);
         }
       }
       seen = __builtin_amdgcn_readfirstlane(seen);
@@ -459,7 +484,7 @@ __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
                   uint8_t* __restrict__ out) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr, 0);
+  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr, 0, 0);
 }
 #endif
 
@@ -561,7 +586,7 @@ __global__ void __launch_bounds__(kThreads, kStagedWavesPerSimd)
 sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
                    uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
                    uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
-                   int* __restrict__ status, uint32_t spin_limit) {
+                   int* __restrict__ status, uint32_t spin_limit, uint32_t poll_gap) {
   __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
   const int lane = lane_id();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -570,7 +595,8 @@ sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows,
     __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
     const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + lane;
     chain_wave(digests, out_stride * 20, f, f < rows, (uint32_t)(cols * 20), (uint32_t)(cols / m),
-               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, status, spin_limit);
+               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, status, spin_limit,
+               poll_gap);
     return;
   }
   const uint64_t nblocks = rows * cols;

@@ -34,6 +34,7 @@ const KnobDef kKnobDefs[K_COUNT] = {
     {"SF_TEST_STAGES", 0},              // K_TEST_STAGES: most column stages of a fused batch (0 = 16)
     {"SF_TEST_MULTI_SELF_GATHER", 0},   // K_TEST_MULTI_SELF_GATHER: one-device multi gather through RCCL (self send/recv)
     {"SF_TEST_CUT_WINDOW_MIB", 0},      // K_TEST_CUT_WINDOW_MIB: sf_index_fd_cut's window (0 = 512 MiB)
+    {"SF_TEST_CHAIN_POLL_GAP_US", 0},   // K_TEST_CHAIN_POLL_GAP_US: wait between a chain lane's polls (0 = s_sleep 8)
 };
 
 std::atomic<int64_t> g_knob[K_COUNT];

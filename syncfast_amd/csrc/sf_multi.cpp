@@ -31,6 +31,7 @@
 
 #include "host_sha1.h"
 #include "sf_internal.hpp"
+#include "../../include/syncfast_amd_test.h"
 
 using namespace sfi;
 
@@ -204,9 +205,59 @@ static int sf_index_file_multi_body(const char* path, uint32_t block_size, uint3
   return SF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Where each device's digests go in one sf_index_device_multi call (the
+// gather plan, exposed to the tests as sf_test_multi_plan): shard r of the
+// file (sf_shard_range) has first_row = its first block and bytes = 20 B per
+// block; the root's rows are hashed straight into the table (kInPlace),
+// every other non-empty shard's into its device's scratch and received by
+// the root at table offset first_row * 20 (kSent); an empty shard takes
+// neither (kNone).  With self_gather (one device, test hook) the only shard
+// is sent too: a self send/recv through RCCL.  The kInPlace and kSent ranges
+// tile [0, nblocks * 20) exactly once.
+enum Route { kNone = 0, kInPlace = 1, kSent = 2 };
+struct ShardPlan {
+  uint64_t start = 0, len = 0, first_row = 0, bytes = 0;
+  Route route = kNone;
+};
+
+void multi_plan(uint64_t file_len, uint32_t bs, uint32_t n, uint32_t root, bool self_gather, ShardPlan* p) {
+  for (uint32_t r = 0; r < n; r++) {
+    shard_of(file_len, bs, n, r, &p[r].start, &p[r].len, &p[r].first_row);
+    p[r].bytes = p[r].len ? ceil_div(p[r].len, bs) * 20 : 0;
+    p[r].route = !p[r].len ? kNone : (r == root && !self_gather) ? kInPlace : kSent;
+  }
+}
+
+// One event per device, recorded on a hash stream for a gather stream to wait
+// on (created on first use, kept; only touched under g_rccl_mu).
+hipEvent_t g_multi_ev[kMaxDevices] = {};
+
+}  // namespace
+
+extern "C" {
+
+int sf_test_multi_plan(uint64_t file_len, uint32_t block_size, uint32_t n_devices, uint32_t root, int self_gather,
+                       uint64_t* table_offset, uint64_t* bytes, int* route) {
+  if (block_size == 0 || n_devices == 0 || n_devices > (uint32_t)kMaxDevices || root >= n_devices || !table_offset ||
+      !bytes || !route)
+    return SF_EINVAL;
+  std::vector<ShardPlan> p(n_devices);
+  multi_plan(file_len, block_size, n_devices, root, self_gather != 0 && n_devices == 1, p.data());
+  for (uint32_t r = 0; r < n_devices; r++) {
+    table_offset[r] = p[r].first_row * 20;
+    bytes[r] = p[r].bytes;
+    route[r] = (int)p[r].route;
+  }
+  return SF_OK;
+}
+
 static int sf_index_device_multi_body(uint32_t n_devices, const void* const* d_shards, uint64_t file_len,
                                       uint32_t block_size, void* const* d_digests, uint32_t root, void* d_table,
-                                      void* const* streams) {
+                                      void* const* streams, void* const* gather_streams) {
   int rc = check_fixed_args(0, block_size);
   if (rc) return rc;
   if (n_devices == 0 || n_devices > (uint32_t)kMaxDevices || root >= n_devices || !d_shards || !d_digests ||
@@ -219,32 +270,42 @@ static int sf_index_device_multi_body(uint32_t n_devices, const void* const* d_s
   }
   if (ndev == 0) return SF_ENODEV;
   if (n_devices > (uint32_t)ndev) return SF_EINVAL;
-  std::vector<uint64_t> start(n_devices), slen(n_devices), first(n_devices);
-  for (uint32_t r = 0; r < n_devices; r++) {
-    shard_of(file_len, block_size, n_devices, r, &start[r], &slen[r], &first[r]);
-    if (slen[r] && (!d_shards[r] || (r != root && !d_digests[r]))) return SF_EINVAL;
-  }
   // SF_TEST_MULTI_SELF_GATHER (test hook): on one device, the shard goes to
   // d_digests[0] and reaches the table through RCCL (a self send/recv), so a
   // one-GPU box exercises the communicator and the grouped exchange.
   const bool self_gather = n_devices == 1 && knob(K_TEST_MULTI_SELF_GATHER) != 0 && d_digests[0];
+  std::vector<ShardPlan> plan(n_devices);
+  multi_plan(file_len, block_size, n_devices, root, self_gather, plan.data());
+  for (uint32_t r = 0; r < n_devices; r++)
+    if (plan[r].route != kNone && (!d_shards[r] || (plan[r].route == kSent && !d_digests[r]))) return SF_EINVAL;
+  auto hs = [&](uint32_t r) { return streams ? as_stream(streams[r]) : nullptr; };
+  auto gs = [&](uint32_t r) { return gather_streams ? as_stream(gather_streams[r]) : hs(r); };
+  const bool exchange = n_devices > 1 || self_gather;
   DeviceGuard g;
-  // 1. every shard hashed on its own device, on its stream; the root's
-  // straight into its place in the table
+  // The whole call under g_rccl_mu when there is an exchange: the per-device
+  // events and the communicators are shared by every call.
+  std::unique_lock<std::mutex> lk(g_rccl_mu, std::defer_lock);
+  if (exchange) lk.lock();
+  // 1. every shard hashed on its own device, on its hash stream; the root's
+  // straight into its place in the table; then the device's gather stream
+  // (when it is another stream) waits for that hashing -- the root's too, so
+  // d_table is complete once gather_streams[root] has run past the call
   for (uint32_t r = 0; r < n_devices; r++) {
-    if (!slen[r]) continue;
+    if (plan[r].route == kNone) continue;
     SF_HIP(hipSetDevice((int)r));
-    uint8_t* dst = r == root && !self_gather ? static_cast<uint8_t*>(d_table) + first[r] * 20
+    uint8_t* dst = plan[r].route == kInPlace ? static_cast<uint8_t*>(d_table) + plan[r].first_row * 20
                                              : static_cast<uint8_t*>(d_digests[r]);
-    if ((rc = launch_fixed(d_shards[r], slen[r], block_size, ceil_div(slen[r], block_size), dst,
-                           streams ? as_stream(streams[r]) : nullptr)) != SF_OK)
-      return rc;
+    if ((rc = launch_fixed(d_shards[r], plan[r].len, block_size, plan[r].bytes / 20, dst, hs(r))) != SF_OK) return rc;
+    if (exchange && gs(r) != hs(r)) {
+      if (!g_multi_ev[r]) SF_HIP(hipEventCreateWithFlags(&g_multi_ev[r], hipEventDisableTiming));
+      SF_HIP(hipEventRecord(g_multi_ev[r], hs(r)));
+      SF_HIP(hipStreamWaitEvent(gs(r), g_multi_ev[r], 0));
+    }
   }
-  if (n_devices == 1 && !self_gather) return SF_OK;
+  if (!exchange) return SF_OK;
   // 2. the gather: every other device sends its table to the root, which
   // receives each at its rows (uneven counts: grouped point-to-point, not
-  // ncclGather), all in one group, stream-ordered after the hashing
-  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  // ncclGather), all in one group, on the gather streams
   std::vector<int> devs(n_devices);
   for (uint32_t r = 0; r < n_devices; r++) devs[r] = (int)r;
   std::vector<ncclComm_t>* comms = nullptr;
@@ -253,12 +314,10 @@ static int sf_index_device_multi_body(uint32_t n_devices, const void* const* d_s
   if (R->group_start() != ncclSuccess) return SF_ENODEV;
   bool ok = true;
   for (uint32_t r = 0; r < n_devices && ok; r++) {
-    if ((r == root && !self_gather) || !slen[r]) continue;
-    const size_t bytes = ceil_div(slen[r], block_size) * 20;
-    ok = R->send(d_digests[r], bytes, ncclUint8, (int)root, (*comms)[r], streams ? as_stream(streams[r]) : nullptr) ==
-             ncclSuccess &&
-         R->recv(static_cast<uint8_t*>(d_table) + first[r] * 20, bytes, ncclUint8, (int)r, (*comms)[root],
-                 streams ? as_stream(streams[root]) : nullptr) == ncclSuccess;
+    if (plan[r].route != kSent) continue;
+    ok = R->send(d_digests[r], plan[r].bytes, ncclUint8, (int)root, (*comms)[r], gs(r)) == ncclSuccess &&
+         R->recv(static_cast<uint8_t*>(d_table) + plan[r].first_row * 20, plan[r].bytes, ncclUint8, (int)r,
+                 (*comms)[root], gs(root)) == ncclSuccess;
   }
   if (R->group_end() != ncclSuccess) ok = false;
   return ok ? SF_OK : SF_ENODEV;
@@ -272,7 +331,17 @@ int sf_index_file_multi(const char* path, uint32_t block_size, uint32_t n_device
 int sf_index_device_multi(uint32_t n_devices, const void* const* d_shards, uint64_t file_len, uint32_t block_size,
                           void* const* d_digests, uint32_t root, void* d_table, void* const* streams) {
   return guarded([&] {
-    return sf_index_device_multi_body(n_devices, d_shards, file_len, block_size, d_digests, root, d_table, streams);
+    return sf_index_device_multi_body(n_devices, d_shards, file_len, block_size, d_digests, root, d_table, streams,
+                                      nullptr);
+  });
+}
+
+int sf_index_device_multi_ex(uint32_t n_devices, const void* const* d_shards, uint64_t file_len, uint32_t block_size,
+                             void* const* d_digests, uint32_t root, void* d_table, void* const* hash_streams,
+                             void* const* gather_streams) {
+  return guarded([&] {
+    return sf_index_device_multi_body(n_devices, d_shards, file_len, block_size, d_digests, root, d_table,
+                                      hash_streams, gather_streams);
   });
 }
 

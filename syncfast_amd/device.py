@@ -21,7 +21,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import FileDesc, check, lib, SF_ERANGE, SF_ETIMEDOUT, SfError
+from ._lib import FileDesc, check, lib, SF_ERANGE, SfError
 
 __all__ = [
     "num_blocks", "index_device", "index_device_blocks", "index_device_batch",
@@ -185,9 +185,9 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
     the digests they consume; a wait that gives up is reported as
     SF_ETIMEDOUT.  With ``status`` (int32[1] on the device, zeroed by the
     caller) the call stays asynchronous and the caller checks it; without,
-    the call synchronises the stream and, on SF_ETIMEDOUT (a backstop, seen
-    once in round 5), runs the batch again on the path that never waits
-    (block kernel, then the chain kernel), so the result is always whole."""
+    the call synchronises the stream and raises SfError(SF_ETIMEDOUT).  The
+    bound is a backstop: the lanes poll with a coherent read (DESIGN.md 3.3;
+    the one time it ran out, round 5, the poll was an L2-served load)."""
     _require_device(data, "data", torch.uint8)
     nf = len(files)
     descs = (FileDesc * max(nf, 1))()
@@ -226,13 +226,7 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
               "sf_index_device_batch")
         if own_status:
             code = int(status.item())
-            if code == SF_ETIMEDOUT:  # a chain lane gave up: the non-waiting path (no status word)
-                check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs,
-                                                  nf, block_size, dig.data_ptr() if total else None,
-                                                  dig.numel() // 20, fh.data_ptr(), first.ctypes.data,
-                                                  ctypes.byref(nb), None, _stream_ptr(data, stream)),
-                      "sf_index_device_batch")
-            elif code != 0:
+            if code != 0:  # SF_ETIMEDOUT: a blocks_hash lane gave up; its hash was not computed
                 raise SfError(code, "sf_index_device_batch")
     return dig, first.astype(np.int64), fh
 
@@ -437,12 +431,18 @@ class BlockSet:
 
 def index_device_multi(shards: Sequence[torch.Tensor], file_len: int, block_size: int, root: int = 0,
                        table: Optional[torch.Tensor] = None, scratch: Optional[Sequence[torch.Tensor]] = None,
-                       streams: Optional[Sequence[torch.cuda.Stream]] = None) -> torch.Tensor:
-    """sf_index_device_multi: shards[r] (on cuda:r) holds shard r
+                       streams: Optional[Sequence[torch.cuda.Stream]] = None,
+                       gather_streams: Optional[Sequence[torch.cuda.Stream]] = None) -> torch.Tensor:
+    """sf_index_device_multi_ex: shards[r] (on cuda:r) holds shard r
     (host.shard_range) of one logical file; every shard is hashed on its own
-    device and the digest tables meet in `table` on cuda:root, gathered over
-    xGMI with RCCL inside the library.  Returns the (nblocks, 20) table,
-    complete once root's stream has run past the call."""
+    device (on streams[r]) and the digest tables meet in `table` on cuda:root,
+    gathered over xGMI with RCCL inside the library (on gather_streams[r],
+    after device r's hashing; default: the hash streams).  Returns the
+    (nblocks, 20) table, complete once gather_streams[root] (or streams[root])
+    has run past the call.  ``streams`` None: each device's default stream.
+    The scratch tables and a table allocated here are marked as in use by the
+    streams the library reads and writes them on, so the caching allocator
+    does not hand them out again before the exchange is done."""
     n = len(shards)
     if n < 1:
         raise ValueError("no shards")
@@ -452,21 +452,34 @@ def index_device_multi(shards: Sequence[torch.Tensor], file_len: int, block_size
         _require_device(t, f"shards[{r}]", torch.uint8, torch.device("cuda", r))
         if t.numel() != shard_range(file_len, block_size, n, r)[1]:
             raise ValueError(f"shards[{r}] is not shard {r} of {n}")
+    for name, ss in (("streams", streams), ("gather_streams", gather_streams)):
+        if ss is not None and (len(ss) != n or any(s.device != torch.device("cuda", r) for r, s in enumerate(ss))):
+            raise ValueError(f"{name}[r] must be a stream of cuda:r, one per shard")
+    hs = list(streams) if streams is not None else [torch.cuda.default_stream(r) for r in range(n)]
+    gs = list(gather_streams) if gather_streams is not None else hs
     dev_root = torch.device("cuda", root)
-    if table is None:
+    own_table = table is None
+    if own_table:
         table = torch.empty((max(nb, 1), 20), dtype=torch.uint8, device=dev_root)
     _require_device(table, "table", torch.uint8, dev_root)
     if table.numel() < nb * 20:
         raise ValueError("table too small")
-    if scratch is None:
+    own_scratch = scratch is None
+    if own_scratch:
         scratch = [torch.empty((max(num_blocks(t.numel(), block_size), 1), 20), dtype=torch.uint8, device=t.device)
                    for t in shards]
     ptr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
-    sp = None
-    if streams is not None:
-        sp = (ctypes.c_void_p * n)(*[s.cuda_stream for s in streams])
-    check(lib().sf_index_device_multi(n, ptr(shards), file_len, block_size, ptr(scratch), root, table.data_ptr(), sp),
-          "sf_index_device_multi")
+    sp = (ctypes.c_void_p * n)(*[s.cuda_stream for s in hs])
+    gp = (ctypes.c_void_p * n)(*[s.cuda_stream for s in gs])
+    check(lib().sf_index_device_multi_ex(n, ptr(shards), file_len, block_size, ptr(scratch), root, table.data_ptr(),
+                                         sp, gp), "sf_index_device_multi_ex")
+    if own_scratch:  # device r's scratch is written on hs[r] and sent on gs[r]
+        for r in range(n):
+            for st in {hs[r], gs[r]}:
+                scratch[r].record_stream(st)
+    if own_table:  # the root's rows are written on hs[root], the others received on gs[root]
+        for st in {hs[root], gs[root]}:
+            table.record_stream(st)
     return table[:nb]
 
 

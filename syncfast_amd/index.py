@@ -69,6 +69,10 @@ log = logging.getLogger("syncfast_amd.index")
 # index_file: times a file that keeps changing while it is indexed
 # (SF_EAGAIN from the descriptor routes) is opened and indexed again.
 CHANGED_RETRIES = 3
+# Index.index_path with a NativeChunker: a file this large is cut on the
+# chunker's threads and hashed from one read (sf_index_fd_cut), not cut on one
+# pool thread among the batch's files (configs[0]'s folder is one 64 MiB file).
+LARGE_FILE_BYTES = 64 << 20
 
 SCHEMA = """
     CREATE TABLE files(
@@ -554,10 +558,13 @@ class Index:
         log.info("File %s keeps changing: indexing the bytes of one read", path)
         self._index_file_once(path, name, force=True, one_pass=True)
 
-    def _index_file_once(self, path, name, force: bool, one_pass: bool = False) -> None:
+    def _index_file_once(self, path, name, force: bool, one_pass: bool = False, opened=None) -> None:
+        """One attempt of index_file; `opened`: the file already open (a FIFO
+        met by the walk is indexed from that open: a second open would wait
+        for another writer, and the first's data would be lost)."""
         ch = self.chunker
         native = None  # (rows, blocks_hash) from a native route
-        with open(path, "rb") as f:  # File::open first: same error on a missing file
+        with (open(path, "rb") if opened is None else opened) as f:  # File::open first: same error on a missing file
             seekable = _seekable(f)
             stamp = host.file_stamp(f.fileno()) if seekable and not one_pass and \
                 (isinstance(ch, FixedChunker) or ch.stream) else None
@@ -613,7 +620,8 @@ class Index:
         self.db.executemany("INSERT INTO blocks(hash, file_id, offset, size, present) VALUES(?, ?, ?, ?, 1);",
                             ((hx[40 * i:40 * i + 40], file_id, offs[i], sizes[i]) for i in range(b - a)))
 
-    def index_path(self, path, batch_bytes: int = 256 << 20, chunk_threads: int = 0) -> None:
+    def index_path(self, path, batch_bytes: int = 256 << 20, chunk_threads: int = 0,
+                   large_file_bytes: int = LARGE_FILE_BYTES) -> None:
         """Index files and directories recursively (src/index.rs:685-715).
 
         Same walk, names and mtime gate as the reference.  With a
@@ -628,8 +636,12 @@ class Index:
         `batch_bytes` of cut files goes through ONE native pipeline
         (sf_index_fds_blocks: the open descriptors re-read by windows into
         packed pinned stages, one sort + one explicit-list launch per stage)
-        while the pool cuts the next batch.  batch_bytes=0 indexes file by
-        file."""
+        while the pool cuts the next batch.  A NativeChunker's files of at
+        least `large_file_bytes` (64 MiB: configs[0]'s one file) are instead
+        cut on `chunk_threads` threads each and hashed from one read
+        (sf_index_fd_cut, Index.index_file's route), in their walk position:
+        one large file alone would otherwise be cut on a single thread.
+        batch_bytes=0 indexes file by file."""
         self._need_chunker()
         todo: List[Tuple[Path, PurePath]] = []
         self._index_path_rec(Path(path), PurePath(""), todo)
@@ -641,7 +653,7 @@ class Index:
             return
         if isinstance(self.chunker, BoundaryChunker):
             if self.chunker.stream:
-                self._index_batched_fds(todo, batch_bytes, chunk_threads)
+                self._index_batched_fds(todo, batch_bytes, chunk_threads, large_file_bytes)
             else:
                 self._index_batched_boundaries(todo, batch_bytes)
             return
@@ -691,7 +703,8 @@ class Index:
             self._insert_rows(file_id, rows, int(first[k]), int(first[k + 1]))
             self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (fhx[40 * k:40 * k + 40], file_id))
 
-    def _index_batched_fds(self, todo, batch_bytes: int, chunk_threads: int) -> None:
+    def _index_batched_fds(self, todo, batch_bytes: int, chunk_threads: int,
+                           large_file_bytes: int = LARGE_FILE_BYTES) -> None:
         """The default (content-defined) mode over many files, the files cut
         in parallel and hashed as ONE pipeline per batch.
 
@@ -702,8 +715,14 @@ class Index:
         the descriptor limit) goes to sf_index_fds_blocks on those same
         descriptors while the pool cuts the next batch.  A file written while
         it was cut or read (SF_EAGAIN for it alone) is indexed again through
-        index_file, in its place, so rows stay in walk order; a FIFO in the
-        tree is indexed through index_file from its own open."""
+        index_file, in its place, so rows stay in walk order.  Two kinds of
+        file are indexed alone, in their walk position, once every batch
+        before them has been stored (rows in walk order, so get_block's first
+        row for a digest is the reference's, src/index.rs:80-90): a FIFO
+        (streamed, as index_file streams it) and, with a NativeChunker, a
+        regular file of at least `large_file_bytes` (cut on the chunker's
+        threads and hashed from one read, sf_index_fd_cut, with the stamp
+        taken at its open)."""
         import resource
         from concurrent.futures import ThreadPoolExecutor
 
@@ -746,18 +765,46 @@ class Index:
 
         prev = None
         batch, futs, nbytes = [], [], 0
+        native = isinstance(ch, NativeChunker)
+
+        def drain():
+            """Store every batch before the file about to be indexed alone."""
+            nonlocal prev, batch, futs, nbytes
+            if prev is not None:
+                p_, prev = prev, None
+                finish(*p_)
+            if batch:
+                b_, f_ = batch, futs
+                batch, futs, nbytes = [], [], 0
+                finish(b_, f_)
+
         pool = ThreadPoolExecutor(max_workers=threads)
         try:
             for p, rel in todo:
                 f = open(p, "rb")  # File::open first: same error on a missing file
                 try:
-                    if not _seekable(f):  # a FIFO: read from its own open, sequentially
-                        f.close()
-                        self.index_file(p, rel)
+                    if not _seekable(f):  # a FIFO: read from this open, sequentially, in its place
+                        drain()
+                        self._index_file_once(p, rel, force=False, opened=f)  # closes f
                         continue
                     stamp = host.file_stamp(f.fileno())
                     file_id, up_to_date = self.add_file(
                         rel, DateTimeUtc.from_ns(stamp.mtime_sec * 10**9 + stamp.mtime_nsec))
+                    if not up_to_date and native and stamp.size >= large_file_bytes > 0:
+                        drain()
+                        try:  # cut on the chunker's threads + hashed, one read of this open
+                            rows_np, bh = host.index_fd_cut(f.fileno(), ch.ops, ch.threads or threads, stamp)
+                        except SfError as e:
+                            if e.code != SF_EAGAIN:
+                                raise
+                            log.info("File %s changed while it was indexed, indexing it again", p)
+                            f.close()
+                            self._index_file_changed(p, rel)
+                            continue
+                        self._insert_rows(file_id, rows_np)
+                        self.db.execute("UPDATE files SET blocks_hash = ? WHERE file_id = ?;", (bh.hex(), file_id))
+                        f.close()
+                        continue
                 except BaseException:
                     f.close()
                     raise

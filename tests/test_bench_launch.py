@@ -99,3 +99,63 @@ def test_config1_probe_reports_toolchain():
     have = shutil.which("cargo") and shutil.which("rustc")
     assert c1["status"] == ("runnable (not timed here)" if have else "reference CPU path not runnable")
     assert set(c1["probe"]) == {"cargo", "rustc", "~/.cargo"}
+
+
+def _plan(*args):
+    r = subprocess.run([sys.executable, BENCH, "--check-plan"] + list(args), capture_output=True, text=True,
+                       timeout=120, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    return _last_json(r.stdout)
+
+
+def test_library_plan_defaults_to_config4_at_n_gt_1():
+    """--gpus N > 1 runs ONE process over N devices through the C-ABI
+    (sf_index_device_multi_ex) on configs[3]'s 32 GiB shard per GPU; the plan
+    (no GPU needed) shards one logical file of N x 32 GiB, block-aligned,
+    with the rows of shard r at its place in the root's table, and rotates the
+    gather's root so the last timed step's table is device 0's."""
+    for n in (2, 8):
+        p = _plan("--gpus", str(n))
+        assert p["path"] == "library" and p["n_devices"] == n and p["config"] == 4
+        assert "configs[3]" in p["workload"] and p["bytes_per_gpu"] == 32 << 30 and p["block_size"] == 4096
+        assert p["total_bytes"] == n * (32 << 30) and p["blocks"] == p["total_bytes"] // 4096
+        pos = 0
+        for r, sh in enumerate(p["shards"]):
+            assert sh["device"] == r and sh["start"] == pos and sh["first_row"] == pos // 4096
+            assert sh["rows"] == (sh["bytes"] + 4095) // 4096
+            pos += sh["bytes"]
+        assert pos == p["total_bytes"]
+        roots = p["roots_timed"]
+        assert len(roots) == 20 and roots[-1] == 0
+        assert max(roots.count(r) for r in range(n)) - min(roots.count(r) for r in range(n)) <= 1
+        assert p["roots_warmup"] == list(range(n))
+
+
+def test_library_plan_uneven_shards_and_one_device():
+    # a shard size that is not a block multiple at an odd device count, and
+    # the one-device library path (the GPU test runs it with the self-gather)
+    p = _plan("--gpus", "3", "--shard-gib", "0.01", "--steps", "7")
+    assert sum(sh["bytes"] for sh in p["shards"]) == p["total_bytes"]
+    assert all(sh["start"] % 4096 == 0 for sh in p["shards"])
+    assert p["roots_timed"][-1] == 0 and len(p["roots_timed"]) == 7
+    one = _plan("--gpus", "1", "--multi-path", "library")
+    assert one["n_devices"] == 1 and one["config"] == 2 and one["shards"][0]["bytes"] == 8 << 30
+
+
+def test_multi_path_resolution():
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+
+    def ns(**kw):
+        base = dict(gpus=1, config=None, multi_path="auto", check_launch=False, dist_backend="nccl")
+        base.update(kw)
+        return bench.resolve_args(argparse.Namespace(**base))
+
+    assert (ns().config, ns().multi_path) == (2, "torch")  # the single-GPU line is unchanged
+    assert (ns(gpus=8).config, ns(gpus=8).multi_path) == (4, "library")
+    assert ns(gpus=8, check_launch=True).multi_path == "torch"
+    assert ns(gpus=2, dist_backend="gloo").multi_path == "torch"
+    assert ns(gpus=8, multi_path="torch").multi_path == "torch"
+    assert ns(gpus=8, config=2).config == 2

@@ -182,27 +182,30 @@ def test_c_consumer_content_defined_wire_run(gpu, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1, 4])
-def test_c_consumer_default_mode_many_files(gpu, tmp_path, threads):
+@pytest.mark.parametrize("threads,large_mib", [(1, 64), (4, 64), (4, 2)])
+def test_c_consumer_default_mode_many_files(gpu, tmp_path, threads, large_mib):
     """examples/sf_index -Z -M: the default mode over many files from C --
     files cut by the stand-in chunker on `threads` threads over their open
     descriptors, batches hashed by sf_index_fds_blocks, two passes in one
-    process.  Every row = the stand-in chunker's boundaries (the oracle's
-    copy of it) with the oracle's digests; every blocks_hash = the oracle's."""
+    process; with -K 2 the files of 2 MiB and more are indexed alone, in
+    their place, through sf_index_fd_cut on the threads.  Every row = the
+    stand-in chunker's boundaries (the oracle's copy of it) with the oracle's
+    digests; every blocks_hash = the oracle's; files in command-line order."""
     exe = _built(False)
     rng = np.random.default_rng(threads)
     paths, datas = [], []
-    for k, n in enumerate([0, 1, 100_000, 32768, 3 << 20, 777] + [int(x) for x in rng.integers(0, 300_000, 40)]):
+    for k, n in enumerate([0, 1, 100_000, 32768, 3 << 20, 777, (9 << 20) + 3] +
+                          [int(x) for x in rng.integers(0, 300_000, 40)] + [2 << 20]):
         p = tmp_path / f"f{k:03d}"
         d = oracle.splitmix_bytes(n, 900 + k)
         d.tofile(p)
         paths.append(str(p))
         datas.append(d)
-    r = subprocess.run([exe, "-Z", "-M", "-P", "2", "-S", "1", "-j", str(threads)] + paths,
+    r = subprocess.run([exe, "-Z", "-M", "-P", "2", "-S", "1", "-K", str(large_mib), "-j", str(threads)] + paths,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     got = _parse(r.stdout)
-    assert sorted(got) == sorted(paths)
+    assert list(got) == paths
     for p, d in zip(paths, datas):
         sizes = oracle.zpaq_standin_sizes(d) if d.size else np.zeros(0, np.uint32)
         offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64) if sizes.size else sizes

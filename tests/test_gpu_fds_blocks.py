@@ -364,9 +364,10 @@ def _standin_ops():
 @pytest.mark.parametrize("n", [0, 1, 70_000, (37 << 20) + 99, (600 << 20) + 5])
 def test_index_fd_cut_equals_oracle(gpu, tmp_path, n):
     """sf_index_fd_cut: the stand-in chunker on 16 threads, the file read once
-    and hashed from HBM (a file over 512 MiB: cut, then hashed from its
-    descriptor); rows and blocks_hash equal the one-stream cut hashed by the
-    oracle, and a stale stamp is SF_EAGAIN."""
+    and hashed from HBM by windows of up to 512 MiB (a 600 MiB file: two
+    windows, the second starting at the first's last boundary); rows and
+    blocks_hash equal the one-stream cut hashed by the oracle, and a stale
+    stamp is SF_EAGAIN."""
     lib, ops = _standin_ops()
     try:
         data = oracle.splitmix_bytes(n, 7700 + n % 97)
@@ -444,5 +445,81 @@ def test_index_fd_cut_small_windows(gpu, tmp_path, knobs, window_mib, n):
                 rows, bh = host.index_fd_cut(f.fileno(), ops, threads)
             assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes), threads
             assert np.array_equal(rows["sha1"], dig) and bh == oracle.blocks_hash(dig), threads
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)
+
+
+def test_index_fd_cut_chunk_longer_than_window(gpu, tmp_path, knobs):
+    """sf_index_fd_cut when a whole window holds no boundary (a chunk longer
+    than the window: here a 1 MiB window and a stand-in with max_size 3 MiB +
+    7 that practically never cuts by content, bits = 32): the call falls back
+    to sf_cut_fd + sf_index_fd_blocks after giving its window buffers back
+    (the fallback used to lease the device cache again while
+    holding it).  Rows = the one-thread cut, digests and blocks_hash = the
+    oracle's, on 1 and 16 threads, twice in a row (the cache is whole after)."""
+    import ctypes
+    knobs.set("SF_TEST_CUT_WINDOW_MIB", 1)
+    lib, ops13 = _standin_ops()
+    ops = lib.sf_zpaq_standin_ops(32, (3 << 20) + 7)
+    try:
+        n = (10 << 20) + 123
+        data = oracle.splitmix_bytes(n, 7760)
+        p = tmp_path / "long"
+        data.tofile(p)
+        with open(p, "rb") as f:
+            offs, sizes = host.cut_fd(f.fileno(), ops, 1)
+        assert int(np.asarray(sizes).max()) > (1 << 20)  # the window holds no boundary
+        offs = np.asarray(offs, np.uint64)
+        sizes = np.asarray(sizes, np.uint32)
+        dig = oracle.index_blocks(data, offs, sizes)
+        for threads in (1, 16, 16):
+            with open(p, "rb") as f:
+                rows, bh = host.index_fd_cut(f.fileno(), ops, threads)
+            assert np.array_equal(rows["offset"], offs) and np.array_equal(rows["size"], sizes), threads
+            assert np.array_equal(rows["sha1"], dig) and bh == oracle.blocks_hash(dig), threads
+    finally:
+        lib.sf_zpaq_standin_ops_free(ctypes.c_void_p(ops))
+        lib.sf_zpaq_standin_ops_free(ops13)
+
+
+def test_index_path_large_file_among_small_files(gpu, tmp_path):
+    """Index.index_path(NativeChunker) over a tree of one 600 MiB file and
+    several hundred small ones (the reference's entry point,
+    src/main.rs:122 -> src/index.rs:685-715 -> :610-659, cut a large file on
+    one thread): the large file goes through sf_index_fd_cut on the chunker's
+    threads in its walk position, the small ones through the batched
+    pipeline.  Every row and blocks_hash equals the oracle's one-stream cut,
+    and the blocks are stored in walk order (file_id non-decreasing by
+    rowid)."""
+    from syncfast_amd.index import Index, NativeChunker
+    lib, ops = _standin_ops()
+    try:
+        root = tmp_path / "t"
+        for d in ("a", "b"):
+            (root / d).mkdir(parents=True)
+        rng = np.random.default_rng(61)
+        datas = {}
+        for k in range(300):
+            n = int(rng.integers(0, 60_000))
+            name = f"{'a' if k % 2 else 'b'}/s{k:03d}"
+            d = oracle.splitmix_bytes(n, 12000 + k)
+            d.tofile(root / name)
+            datas[name] = d
+        big = oracle.splitmix_bytes((600 << 20) + 5, 12999)
+        big.tofile(root / "a" / "big")
+        datas["a/big"] = big
+        idx = Index.open_in_memory(chunker=NativeChunker(ops, threads=16))
+        idx.index_path(root)
+        for name, d in datas.items():
+            fid, _, bh = idx.get_file(name)
+            rows = idx.list_file_blocks(fid)
+            sizes = oracle.zpaq_standin_sizes(d).astype(np.uint32)
+            offs = _offs(sizes)
+            dig = oracle.index_blocks(d, offs, sizes) if sizes.size else np.zeros((0, 20), np.uint8)
+            assert [(o, s) for _h, o, s in rows] == list(zip(offs.tolist(), sizes.tolist())), name
+            assert [h.to_sql() for h, _o, _s in rows] == [bytes(x).hex() for x in dig], name
+            assert bh.to_sql() == oracle.blocks_hash(dig).hex(), name
+        fids = [r[0] for r in idx.db.execute("SELECT file_id FROM blocks ORDER BY rowid")]
+        assert fids == sorted(fids)
     finally:
         lib.sf_zpaq_standin_ops_free(ops)

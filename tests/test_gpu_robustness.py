@@ -2,12 +2,16 @@
 
 - The fused many-file launch (sha1_staged_kernel): its blocks_hash lanes wait
   (bounded) for block digests; a wait that gives up must surface as
-  SF_ETIMEDOUT in the caller's status word, never as an all-zero blocks_hash
-  with rc = 0 (the reference never yields a hash it did not compute,
-  src/index.rs:661-682); sf_index_files never takes the waiting path, and the
-  Python wrapper without a status word reruns on the path that does not
-  wait.  Forced with
-  SF_TEST_CHAIN_SPIN_LIMIT=0 (one poll per wait; test hook).
+  SF_ETIMEDOUT in the caller's status word (or SfError from the Python
+  wrapper), never as an all-zero blocks_hash with rc = 0 (the reference never
+  yields a hash it did not compute, src/index.rs:661-682); sf_index_files
+  never takes the waiting path.  Forced with SF_TEST_CHAIN_SPIN_LIMIT=0 (one
+  poll per wait; test hook).
+- The lanes' poll sees every XCD's arrivals: a lane whose first poll comes
+  before the block waves finish and whose next comes after they all have
+  (SF_TEST_CHAIN_POLL_GAP_US) completes at the default bound, and the XCD
+  litmus (sf_test_xcd_litmus) shows the poll's read-modify-write seeing adds
+  made on other XCDs after its XCD's L2 holds the line.
 - Batches too wide for the fused launch's chain workgroups to stay below the
   resident capacity, and callers without a status word, take the non-waiting
   path: correct hashes even with the spin limit at 0.
@@ -36,20 +40,56 @@ def _equal_batch(gpu, nfiles, nbf, bs, seed):
     return data, t, files
 
 
-def test_staged_chain_timeout_is_reported_or_recovered(gpu, knobs):
+def test_staged_chain_timeout_is_reported(gpu, knobs):
     knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
     data, t, files = _equal_batch(gpu, 64, 1024, 4096, 501)  # 256 MiB: stage 0 cannot be done at the first poll
     # the asynchronous form: the caller's status word carries it
     st = torch.zeros(1, dtype=torch.int32, device=gpu)
     device.index_device_batch(t, files, 4096, status=st)
     assert int(st.item()) == SF_ETIMEDOUT
-    # without one, the wrapper runs the batch again on the non-waiting path
-    dig, _, fh = device.index_device_batch(t, files, 4096)
+    # without one, the wrapper raises: no hash it did not compute, no rerun
+    with pytest.raises(SfError) as e:
+        device.index_device_batch(t, files, 4096)
+    assert e.value.code == SF_ETIMEDOUT
+
+
+@pytest.mark.parametrize("gap_us", [50_000, 20])
+def test_staged_poll_after_every_block_wave_finished(gpu, knobs, gap_us):
+    # A lane's first poll of stage 0 comes right at the launch's start (the
+    # chain workgroups are dispatched first), before the stage is done; with a
+    # 50 ms gap its next poll comes after every block wave of the 256 MiB
+    # launch has finished, when no XCD adds to the counters any more (the
+    # window in which an L2-served load of the counter line stays stale);
+    # with 20 us it polls many times while they run.  The default bound
+    # holds either way and every blocks_hash is the oracle's.
+    knobs.set("SF_TEST_CHAIN_POLL_GAP_US", gap_us)
+    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 508)
+    st = torch.zeros(1, dtype=torch.int32, device=gpu)
+    dig, _, fh = device.index_device_batch(t, files, 4096, status=st)
+    assert int(st.item()) == 0
     want = oracle.index_fixed_mt(data, 4096, 8)
     assert np.array_equal(dig.cpu().numpy(), want)
     fhn = fh.cpu().numpy()
-    for i in (0, 17, 63):
+    for i in range(64):
         assert bytes(fhn[i]) == oracle.blocks_hash(want[i * 1024:(i + 1) * 1024]), i
+
+
+def test_xcd_counter_litmus(gpu):
+    # The poll's read-modify-write (mode 1) returns every add made on other
+    # XCDs after the reader's first read put the counter's line in its XCD's
+    # L2.  Mode 0 (the relaxed atomic load the poll used until round 6) is run
+    # and reported; its outcome is the hardware's, recorded in DESIGN.md 3.3
+    # (scripts/xcd_litmus.py), so only its hand-shake is asserted here.
+    torch.cuda.set_device(gpu)
+    for mode in (1, 0, 1, 0):
+        out = (ctypes.c_uint32 * 8)()
+        assert lib().sf_test_xcd_litmus(mode, out) == 0
+        status, xcc, adders, v0, v1, fresh = list(out)[:6]
+        assert status == 0 and adders > 0 and v0 == 0, list(out)
+        assert fresh == adders, list(out)  # the read-modify-write read sees every add
+        if mode == 1:
+            assert v1 == adders, list(out)
+        print(f"litmus mode {mode}: reader XCD {xcc}, {adders} adds from other XCDs, second read {v1}")
 
 
 def test_staged_default_spin_limit_is_green(gpu):

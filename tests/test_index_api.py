@@ -706,3 +706,70 @@ def test_native_chunker_matches_the_python_chunker(tmp_path, monkeypatch):
         assert nc.fn(io.BytesIO(data.tobytes())) == oracle.zpaq_standin_sizes(data).tolist()
     finally:
         lib.sf_zpaq_standin_ops_free(ops)
+
+
+@pytest.mark.timeout(120)
+def test_index_path_large_files_and_fifo_keep_walk_order(tmp_path, monkeypatch):
+    """Index.index_path with a NativeChunker: files of at least
+    large_file_bytes are cut on the chunker's threads and hashed from one read
+    (sf_index_fd_cut; the oracle stands in for the device) in their walk
+    position, a FIFO is streamed from its own open, and both wait for every
+    batch before them to be stored: the files and the blocks, in rowid order,
+    are exactly what the file-by-file walk stores (get_block returns the first
+    row for a digest, src/index.rs:80-90, so the order is observable)."""
+    import threading
+    from syncfast_amd import host
+    from syncfast_amd.index import NativeChunker
+    _oracle_device_calls(monkeypatch)
+    calls = []
+
+    def fd_cut(fd, ops, threads=0, stamp=None):
+        calls.append(os.fstat(fd).st_size)
+        offs, sizes = host.cut_fd(fd, ops, threads, stamp)
+        raw = _pread_all(fd)
+        rows = np.zeros(offs.size, host.SIG_DTYPE)
+        rows["offset"], rows["size"] = offs, sizes
+        dig = oracle.index_blocks(np.frombuffer(raw, np.uint8), offs, sizes) if offs.size else np.zeros((0, 20), np.uint8)
+        rows["sha1"] = dig
+        return rows, oracle.blocks_hash(dig)
+
+    monkeypatch.setattr(host, "index_fd_cut", fd_cut)
+    lib = _standin_ops_lib()
+    ops = lib.sf_zpaq_standin_ops(13, 32768)
+    root = tmp_path / "tree"
+    (root / "sub").mkdir(parents=True)
+    sizes = [40_000, 3_000, (2 << 20) + 17, 90_000, 0, 55_555, (1 << 20), 12_000, 70_000, 1, 33_000, 64_000]
+    for k, n in enumerate(sizes):
+        # the same bytes twice (k and k + 6): duplicate digests across files
+        (root / ("sub" if k % 3 == 0 else ".") / f"f{k:02d}").write_bytes(
+            oracle.splitmix_bytes(n, 9900 + k % 6).tobytes())
+    fifo = root / "pipe"
+    os.mkfifo(fifo)
+    fdata = oracle.splitmix_bytes(100_000, 9950).tobytes()
+
+    second = threading.Event()
+
+    def writer():  # one writer per reader's open (a writer reopening at once could meet the last reader)
+        for k in range(2):
+            if k:
+                second.wait(60)
+            with open(fifo, "wb") as w:
+                w.write(fdata)
+
+    th = threading.Thread(target=writer, daemon=True)
+    th.start()
+    try:
+        ref = Index.open_in_memory(chunker=NativeChunker(ops, threads=4))
+        ref.index_path(root, batch_bytes=0)
+        second.set()
+        calls.clear()
+        got = Index.open_in_memory(chunker=NativeChunker(ops, threads=4))
+        got.index_path(root, batch_bytes=100_000, chunk_threads=3, large_file_bytes=1 << 20)
+        th.join(timeout=30)
+        assert sorted(calls) == [1 << 20, (2 << 20) + 17]  # the two large files, nothing else
+        for q in ("SELECT file_id, name, blocks_hash FROM files ORDER BY file_id",
+                  "SELECT file_id, hash, offset, size, present FROM blocks ORDER BY rowid"):
+            assert got.db.execute(q).fetchall() == ref.db.execute(q).fetchall(), q
+        assert got.get_file("pipe") is not None
+    finally:
+        lib.sf_zpaq_standin_ops_free(ops)
