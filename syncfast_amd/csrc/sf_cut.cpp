@@ -275,13 +275,24 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   // takes a lease of its own (a nested lease would try_lock the device's
   // cache mutex this thread already owns)
   auto res = std::make_unique<HostLease>();
-  hipStream_t* st;
-  hipEvent_t* done_ev;
-  uint8_t *pin = nullptr, *dwin = nullptr;
+  hipStream_t* st;  // st[0]: the window's copies to HBM; st[1]: list upload, kernel, digests back
+  hipEvent_t* done_ev;  // done_ev[w & 1]: window w's digests are in host memory
+  uint8_t *pin = nullptr, *dwin[2] = {nullptr, nullptr};
+  const uint64_t wbytes = std::min(len, W);
   int rc = res->streams(st, done_ev);
-  if (rc == SF_OK) rc = res->pin(0, std::min(len, W), reinterpret_cast<void**>(&pin));
-  if (rc == SF_OK) rc = res->dev(0, std::min(len, W), reinterpret_cast<void**>(&dwin));
+  if (rc == SF_OK) rc = res->pin(0, wbytes, reinterpret_cast<void**>(&pin));
+  // two device windows: window w + 1 is read and copied while window w's
+  // chunks are hashed (its device work overlaps the next window's cutting)
+  if (rc == SF_OK) rc = res->dev(0, wbytes, reinterpret_cast<void**>(&dwin[0]));
+  if (rc == SF_OK && len > W) rc = res->dev(1, wbytes, reinterpret_cast<void**>(&dwin[1]));
   if (rc != SF_OK) return rc;
+  struct Ev {  // window w's copies to HBM are done (the pinned window may be refilled)
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } copied;
+  SF_HIP(hipEventCreateWithFlags(&copied.e, hipEventDisableTiming));
   const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
   const auto t0 = std::chrono::steady_clock::now();
   auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
@@ -295,14 +306,46 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   std::atomic<bool> copy_failed{false};
   for (auto& o : seg_owner) o.store(nullptr, std::memory_order_relaxed);
   std::vector<uint64_t> ends;
+  // A window whose chunks are on the device: where it starts, how many, and
+  // the pinned list (offsets then sizes) and digests its rows come from.
+  struct Pending {
+    bool on = false;
+    uint64_t A = 0, n = 0;
+    const uint8_t* plist = nullptr;
+    const uint8_t* pdig = nullptr;
+  } pend[2];
+  // rows + blocks_hash of window w, in window order, once its digests are back
+  auto harvest = [&](uint64_t w) -> int {
+    Pending& p = pend[w & 1];
+    if (!p.on) return SF_OK;
+    const double d0 = ms();
+    SF_HIP(hipEventSynchronize(done_ev[w & 1]));
+    t_dev += ms() - d0;
+    const uint64_t* lo = reinterpret_cast<const uint64_t*>(p.plist);
+    const uint32_t* lz = reinterpret_cast<const uint32_t*>(lo + p.n);
+    const size_t r0 = rows_v.size();
+    rows_v.resize(r0 + p.n);
+    for (uint64_t j = 0; j < p.n; j++) {
+      rows_v[r0 + j].offset = p.A + lo[j];
+      rows_v[r0 + j].size = lz[j];
+      memcpy(rows_v[r0 + j].sha1, p.pdig + 20 * j, 20);
+    }
+    sf_host_sha1_update(&bh, p.pdig, p.n * 20);  // compute_blocks_hash (src/index.rs:661-682), in order
+    p.on = false;
+    return SF_OK;
+  };
   // Window by window: bytes [A, B) read once into the pinned window by the
   // threads that cut them (a segment each, its copy to HBM started at once),
   // cut and joined; the chunks a boundary closes inside the window are hashed
   // from HBM, and the next window starts at the last of those boundaries (the
-  // chunk running over B is cut again from there).
-  for (uint64_t A = 0; A < len || (len == 0 && A == 0);) {
+  // chunk running over B is cut again from there).  Window w's list upload,
+  // kernel and digests run on st[1] while window w + 1 is read and cut; its
+  // rows are taken after that cut (harvest), so rows stay in file order.
+  uint64_t w = 0;
+  for (uint64_t A = 0; A < len || (len == 0 && A == 0); w++) {
     const uint64_t B = std::min(len, A + W);
     const bool eof = B == len;
+    uint8_t* const dw = dwin[w & 1];
     const uint64_t k = seg_count(A, B, threads);
     if (k > nseg_max) return SF_EINVAL;
     const uint64_t seg_len = std::max<uint64_t>(1, (B - A) / k);
@@ -327,7 +370,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
       if (!p) return nullptr;
       if (own != want) memcpy(pin + (pos - A), p, own);
       // the piece's copy to HBM starts now, while the chunker cuts it
-      if (hipMemcpyAsync(dwin + (pos - A), pin + (pos - A), own, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
+      if (hipMemcpyAsync(dw + (pos - A), pin + (pos - A), own, hipMemcpyHostToDevice, st[0]) != hipSuccess) {
         (void)hipGetLastError();
         copy_failed.store(true, std::memory_order_relaxed);
         return nullptr;
@@ -354,8 +397,12 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     t_cut += ms() - c0;
     if (rc == SF_EIO && stamp_of(fd, &after, nullptr) && !same_stamp(before, after)) rc = SF_EAGAIN;
     if (rc != SF_OK) return rc;
+    // the window's copies are queued on st[0]; the pinned window is refilled
+    // only once they are done (below, before the next window's cut)
+    SF_HIP(hipEventRecord(copied.e, st[0]));
     if (!eof && ends.empty()) {  // no boundary in a whole window (a chunk longer than W): two calls
       SF_HIP(hipStreamSynchronize(st[0]));
+      SF_HIP(hipStreamSynchronize(st[1]));
       res.reset();  // the window's buffers and streams go back before sf_index_fd_blocks leases them
       uint64_t *o = nullptr, n = 0;
       uint32_t* z = nullptr;
@@ -372,51 +419,55 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
       *n_out = n;
       return SF_OK;
     }
-    // hash the window's chunks: one launch over its bytes already in HBM
+    // the previous window's rows (its device work ran during this cut)
+    if (w > 0 && (rc = harvest(w - 1)) != SF_OK) return rc;
+    // hash the window's chunks: one launch over its bytes in HBM, on st[1]
+    // after the window's copies
     const uint64_t n = ends.size();
-    const double d0 = ms();
     if (n) {
       uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
       const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
-      if ((rc = res->pin(5, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
-          (rc = res->dev(5, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
-          (rc = res->pin(3, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
-          (rc = res->dev(3, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
+      const int b = (int)(w & 1);
+      if ((rc = res->pin(5 + b, lbytes, reinterpret_cast<void**>(&plist))) != SF_OK ||
+          (rc = res->dev(5 + b, lbytes, reinterpret_cast<void**>(&dlist))) != SF_OK ||
+          (rc = res->pin(3 + b, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
+          (rc = res->dev(3 + b, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
         return rc;
       uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
       uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);
-      for (uint64_t j = 0, b = A; j < n; b = ends[j], j++) {
-        if (ends[j] - b > 0xFFFFFFFFull) return SF_EINVAL;
-        lo[j] = b - A;  // offsets in the window
-        lz[j] = (uint32_t)(ends[j] - b);
+      for (uint64_t j = 0, e = A; j < n; e = ends[j], j++) {
+        if (ends[j] - e > 0xFFFFFFFFull) return SF_EINVAL;
+        lo[j] = e - A;  // offsets in the window
+        lz[j] = (uint32_t)(ends[j] - e);
       }
-      SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[0]));
+      SF_HIP(hipStreamWaitEvent(st[1], copied.e, 0));
+      SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[1]));
       const uint64_t* d_off = reinterpret_cast<const uint64_t*>(dlist);
-      if ((rc = launch_table(dwin, B - A, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
-                             st[0])) != SF_OK)
+      if ((rc = launch_table(dw, B - A, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
+                             st[1])) != SF_OK)
         return rc;
-      SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[0]));
-      SF_HIP(hipStreamSynchronize(st[0]));  // also: the window's copies are done before it is refilled
-      const size_t r0 = rows_v.size();
-      rows_v.resize(r0 + n);
-      for (uint64_t j = 0; j < n; j++) {
-        rows_v[r0 + j].offset = A + lo[j];
-        rows_v[r0 + j].size = lz[j];
-        memcpy(rows_v[r0 + j].sha1, pdig + 20 * j, 20);
-      }
-      sf_host_sha1_update(&bh, pdig, n * 20);  // compute_blocks_hash (src/index.rs:661-682), in order
-    } else {
-      SF_HIP(hipStreamSynchronize(st[0]));
+      SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[1]));
+      SF_HIP(hipEventRecord(done_ev[b], st[1]));
+      pend[b].on = true;
+      pend[b].A = A;
+      pend[b].n = n;
+      pend[b].plist = plist;
+      pend[b].pdig = pdig;
     }
-    t_dev += ms() - d0;
     if (eof) break;
     A = ends.back();
+    // the next window is read into the pinned window: this window's copies
+    // out of it must be done (they ran while it was cut; this waits for the tail)
+    const double d0 = ms();
+    SF_HIP(hipEventSynchronize(copied.e));
+    t_dev += ms() - d0;
   }
+  if ((rc = harvest(w)) != SF_OK) return rc;  // the last window
   if (!stamp_of(fd, &after, nullptr)) return SF_EIO;
   if (!same_stamp(before, after)) return SF_EAGAIN;  // written while read: not one version's rows
   if (trace)
-    fprintf(stderr, "sf_index_fd_cut trace: %llu B, %zu blocks: cut+join %.3f, device %.3f, total %.3f ms\n",
-            (unsigned long long)len, rows_v.size(), t_cut, t_dev, ms());
+    fprintf(stderr, "sf_index_fd_cut trace: %llu B, %zu blocks, %llu windows: cut+join %.3f, waits %.3f, total %.3f ms\n",
+            (unsigned long long)len, rows_v.size(), (unsigned long long)(w + 1), t_cut, t_dev, ms());
   sf_block_sig* out = static_cast<sf_block_sig*>(malloc((rows_v.empty() ? 1 : rows_v.size()) * sizeof(sf_block_sig)));
   if (!out) return SF_ENOMEM;
   if (!rows_v.empty()) memcpy(out, rows_v.data(), rows_v.size() * sizeof(sf_block_sig));
