@@ -50,7 +50,7 @@ extern "C" {
 #define SF_EINVAL (-22)  /* bad argument */
 #define SF_ENOSPC (-28)  /* output capacity too small; *n_out holds the need */
 #define SF_ERANGE (-34)  /* a block lies outside [0, len) */
-#define SF_ETIMEDOUT (-110) /* a device-side wait gave up; the affected blocks_hash values are invalid */
+#define SF_ETIMEDOUT (-110) /* kept for callers: no call returns it since round 6 (no kernel waits) */
 
 /* One signature row: what index_file passes to add_block
  * (src/index.rs:636-642) and what FILE_BLOCK carries on the wire
@@ -119,13 +119,15 @@ int sf_index_device_blocks_weak(const void *d_data, uint64_t len, const uint64_t
  * device.  first_block (host, n_files+1 entries, may be NULL) receives the
  * index of each file's first digest row; *n_blocks the total.  Asynchronous
  * on `stream` (ragged batches upload a small block table, stream-ordered).
- * d_status (device int32, caller-initialised to 0, may be NULL): equal-size
- * batches with d_file_hashes run ONE fused launch whose blocks_hash lanes
- * wait (bounded) for the block digests they consume; if a wait gives up,
- * those files' hashes are zeroed and *d_status is set to SF_ETIMEDOUT --
- * the caller must check it before using d_file_hashes.  With d_status ==
- * NULL the batch takes the non-waiting path (block kernel, then a chain
- * kernel), which cannot time out. */
+ * Equal-size batches with d_file_hashes are hashed in two column halves, the
+ * first half of every file's blocks_hash chain beside the second half's
+ * blocks, then the chains' second half (the batch stream's last batch,
+ * sf_index_device_batch_chained_cols): no wave waits for another, so no
+ * bound and no timeout (round 6; until then one fused launch whose chain
+ * lanes polled and, once, gave up).  d_status (device int32, may be NULL) is
+ * accepted for source compatibility and is not written: no error of this
+ * call is reported on the device.  (SF_BATCH_FUSED=0: the block kernel, then
+ * a chain kernel.) */
 int sf_index_device_batch(const void *d_data, uint64_t len, const sf_file_desc *files,
                           uint32_t n_files, uint32_t block_size, void *d_digests,
                           uint64_t cap_blocks, void *d_file_hashes, uint64_t *first_block,
@@ -360,9 +362,8 @@ void sf_free_rows(sf_block_sig *rows);
  * blocks_hashes: 20 B per file.  *n_out = total rows (the need, with
  * SF_ENOSPC, checked before any file is read).  On SF_EIO (open, stat or a
  * short read: the file changed while being indexed) *bad_file (may be NULL)
- * is the index of the failing file.  Each stage's blocks take the batch path
- * that never waits (sf_index_device_batch with no status word): the call
- * never returns SF_ETIMEDOUT.  Blocking. */
+ * is the index of the failing file.  Each stage's blocks and blocks_hash
+ * chains go through sf_index_device_batch.  Blocking. */
 int sf_index_files(const char *const *paths, uint32_t n_files, uint32_t block_size, uint64_t stage_bytes,
                    sf_block_sig *out, uint64_t cap, uint64_t *first_row, uint8_t *blocks_hashes,
                    uint64_t *n_out, uint32_t *bad_file);

@@ -64,9 +64,9 @@ int sf_test_multi_plan(uint64_t file_len, uint32_t block_size, uint32_t n_device
 
 /* Cross-XCD counter litmus (sf_litmus.hip): does a read of a counter see
  * adds made on other XCDs after the reading XCD's L2 holds its line?
- * mode 0 reads with a relaxed agent-scope atomic load, mode 1 with an
- * agent-scope atomic add of an opaque zero (the fused launch's poll,
- * sf_kernels.hpp coherent_read_u32).  One launch on the current device,
+ * mode 0 reads with a relaxed agent-scope atomic load (round 5's fused
+ * launch polled that way), mode 1 with an agent-scope atomic add of an
+ * opaque zero.  One launch on the current device,
  * synchronous.  out[8]: status (0 ok, 1 a hand-shake wait ran out), the
  * reader's XCD id, adds made from other XCDs, first read, read after every
  * add returned, a read-modify-write read after that, mode, 0.  A stale form

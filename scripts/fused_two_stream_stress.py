@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Fused many-file launches (sf_index_device_batch with a status word:
-sha1_staged_kernel, blocks_hash lanes polling stage counters) alternating on
+sha1_staged_kernel with its blocks_hash chains) alternating on
 two streams with nothing between them -- the pattern of round 5's
-sf_index_files stages when its one SF_ETIMEDOUT happened.
-Each launch's counters come from hipMallocAsync on its stream and go back with
+sf_index_files stages when its one SF_ETIMEDOUT happened (run in
+round 6 on the waiting form, 2000 launches without a timeout, and kept for the
+no-wait form, whose status word is never written).
+Each launch's counter words come from hipMallocAsync on its stream and go back with
 hipFreeAsync behind the kernel, so this also exercises the stream-ordered
 allocator handing one launch's freed counters to the other stream's next
 launch.  Every status word must stay 0 and every blocks_hash equal the
@@ -22,12 +24,10 @@ def main():
     ap.add_argument("--launches", type=int, default=400)
     ap.add_argument("--files", type=int, default=32)
     ap.add_argument("--file-mib", type=int, default=8)
-    ap.add_argument("--spin-limit", type=int, default=1 << 20)
     a = ap.parse_args()
     import numpy as np
     import torch
-    from syncfast_amd import _lib, device, host
-    _lib.set_knob("SF_TEST_CHAIN_SPIN_LIMIT", a.spin_limit)  # a stuck lane gives up in well under a second
+    from syncfast_amd import device, host
     dev = torch.device("cuda", 0)
     flen = a.file_mib << 20
     data = [device.splitmix_tensor(a.files * flen, 4242 + k, device=dev) for k in range(2)]
@@ -54,7 +54,7 @@ def main():
         fh = fhs[k].cpu().numpy()
         for f in (0, a.files // 2, a.files - 1):
             ok_hashes &= bytes(fh[f]) == host.blocks_hash(d[f])
-    print(json.dumps({"launches": a.launches, "files": a.files, "file_mib": a.file_mib, "spin_limit": a.spin_limit,
+    print(json.dumps({"launches": a.launches, "files": a.files, "file_mib": a.file_mib,
                       "nonzero_status": bad, "first_bad": [int(x) for x in np.nonzero(st)[0][:10]],
                       "status_values": sorted(set(int(x) for x in st)), "last_hashes_ok": bool(ok_hashes),
                       "seconds": round(dt, 3)}), flush=True)

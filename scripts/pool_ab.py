@@ -8,7 +8,9 @@ files in the page cache:
   fds      sf_index_fds_blocks over the small tree, CDC-like lists
 Each library runs in its own process (SF_LIB), interleaved, REPS rounds.
 
-usage: python scripts/pool_ab.py NAME=LIB [NAME=LIB ...]
+usage: python scripts/pool_ab.py NAME=LIB[,KNOB=VALUE...] [NAME=LIB ...]
+       (round 6: the same library with SF_BATCH_FUSED=1 / 0, the fused
+       many-file launch against blocks-then-chains inside sf_index_files)
        python scripts/pool_ab.py --child DIR   (one library, one JSON line)"""
 import json
 import os
@@ -103,9 +105,11 @@ def main():
         json.dump(write_tree(d), open(os.path.join(d, "tree.json"), "w"))
         for r in range(reps):
             order = libs[r % len(libs):] + libs[:r % len(libs)]
-            for name, lib in order:
+            for name, spec in order:
+                lib, *kv = spec.split(",")
+                env = dict(os.environ, SF_LIB=os.path.abspath(lib), **dict(x.split("=", 1) for x in kv))
                 out = subprocess.run([sys.executable, __file__, "--child", d], capture_output=True, text=True,
-                                     env=dict(os.environ, SF_LIB=os.path.abspath(lib)), timeout=300)
+                                     env=env, timeout=300)
                 line = out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-300:]
                 print(json.dumps({"round": r, "lib": name, "GB/s": line}), flush=True)
     finally:

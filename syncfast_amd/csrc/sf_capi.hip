@@ -186,46 +186,39 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
 }
 
 // Many equal-size, block-aligned files back to back, with their per-file
-// blocks_hash.  Staged (S > 1): ONE launch of sha1_staged_kernel whose first
-// workgroups run the per-file chains while the others hash the blocks in S
-// column stages; only the last stage's chain work follows the last block.
-// Unstaged: the block kernel, then the stand-alone chain kernel.
-//
-// The chain waves wait on block waves, so the staged launch needs (a) block
-// workgroups to find free slots while every chain workgroup is resident and
-// (b) somewhere to report a chain that gave up.  (a): the chain workgroups
-// are kept to at most one per CU (a quarter of the staged kernel's 4
-// workgroups per CU); larger batches (> 256 x 256 files) take the unstaged
-// path, which never waits.  (b): d_status (device int32) receives
-// SF_ETIMEDOUT; with d_status == NULL the unstaged path is taken.
-// SF_TEST_CHAIN_SPIN_LIMIT (test hook) bounds the polls of each wait
-// (default 2^24, several seconds): a backstop, since the poll is a coherent
-// read (sf_kernels.hpp, coherent_read_u32).
-
-inline uint32_t chain_spin_limit() {
-  const int64_t v = knob(K_TEST_CHAIN_SPIN_LIMIT);
-  return v >= 0 ? (uint32_t)std::min<int64_t>(v, 0xFFFFFFFFll) : (1u << 24);
-}
-// SF_TEST_CHAIN_POLL_GAP_US (test hook): a chain lane whose poll did not match
-// waits this long (100 MHz wall-clock ticks) before the next, so a test can
-// put a lane's first poll before the block waves finish and its next after.
-inline uint32_t chain_poll_gap() {
-  const int64_t v = knob(K_TEST_CHAIN_POLL_GAP_US);
-  return v > 0 ? (uint32_t)std::min<int64_t>(v * 100, 0xFFFFFFFFll) : 0u;
-}
-
-int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
-                 uint8_t* fh, int* d_status, hipStream_t s) {
-  int S = 1;
-  const int64_t sk = knob(K_TEST_STAGES);  // SF_TEST_STAGES (test hook); default up to 16 stages
-  const int smax = sk > 0 ? (int)std::min<int64_t>(sk, 32) : 16;
-  for (int cand : {32, 16, 8, 4, 2})
-    if (cand <= smax && nbf % (64ull * cand) == 0 && ((uint64_t)nfiles * (nbf / cand)) % 64 == 0) {
-      S = cand;
-      break;
-    }
-  if (!d_status || ceil_div(nfiles, 64 * sf::kWavesPerWG) > device_cus() || nbf * nfiles > launch_max_blocks()) S = 1;
-  if (S == 1) {
+// blocks_hash (src/index.rs:661-682), and no wave waiting for another
+// (round 6).  A file's blocks_hash is one sequential SHA-1 over its digest
+// run, which exists only once its blocks are hashed; the batch is therefore
+// hashed as the batch stream hashes its last batch, from
+// this stream's pieces (sf_stream.hip, sf_chain.hip):
+//   1. block columns [0, cut) of every file (sha1_fixed_chained_kernel, no jobs);
+//   2. columns [cut, nbf) beside the FIRST half of every file's chain (its
+//      digests [0, cut) exist: launch 1 finished them), the SHA-1 state kept
+//      in HBM;
+//   3. the second half of every chain alone, with schedule-building helper
+//      waves (sha1_chain_helper_kernel).
+// Round 5's single fused launch (sha1_staged_kernel: chain lanes polling
+// per-stage counters, bounded) gave up once in five rounds for a reason no
+// probe reproduced; this form runs config 3's shape at 2.76
+// ms per 8 GiB against that launch's 2.71 and 2.97 for blocks-then-chains
+// (profiles/r06/batch/).  Other shapes (runs not 16-B aligned, fewer than 128
+// blocks per file, not a multiple of 64 or more than 16,384, SF_BATCH_FUSED=0):
+// the block kernel, then the chain kernel.  d_status is not written.
+int batch_with_hashes(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfiles, uint64_t nbf, uint8_t* dig,
+                      uint8_t* fh, bool halves, hipStream_t s) {
+  uint64_t cut = 0;
+  // Files of more than 16,384 blocks (64 MiB at 4 KiB): chains of over 5,120
+  // compressions run faster whole and alone with their helper waves than half
+  // beside the blocks (64 x 128 MiB: 11.5 ms that way, 12.4 in halves; 16 x
+  // 512 MiB 37.2 against 44.0; 256 x 32 MiB the other way, 4.89 against 4.28).
+  if (halves && nbf % 64 == 0 && nbf >= 128 && nbf <= 16384 && (reinterpret_cast<uintptr_t>(dig) & 15) == 0 &&
+      nbf * nfiles <= launch_max_blocks()) {
+    const uint64_t half = (nbf * 20 / 64) / 2;  // data chunks of part 1 (as the chained launcher cuts them)
+    const uint64_t need = ceil_div(half * 64, 20);  // digests part 1 reads
+    cut = ceil_div(need, 64) * 64;                  // in whole block waves
+    if (cut >= nbf) cut = 0;
+  }
+  if (!cut) {
     int rc = launch_fixed(base, nbf * nfiles * (uint64_t)bs, bs, nbf * nfiles, dig, s);
     if (rc) return rc;
     if (nbf % 4 == 0 && nbf * 20 <= 0xFFFFFFF0ull && (reinterpret_cast<uintptr_t>(dig) & 15) == 0) {
@@ -246,20 +239,14 @@ int batch_staged(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t nfile
                        nfiles, (uint32_t)(nbf * 20), fh);
     return hip_err(hipGetLastError());
   }
-  const uint64_t m = nbf / S;
-  const sf::PadSchedule pad = pad_schedule(bs);
-  uint32_t* words = nullptr;  // [0, 32): stage counters
-  const size_t wbytes = 32 * sizeof(uint32_t);
-  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&words), wbytes, s));
-  SF_HIP(hipMemsetAsync(words, 0, wbytes, s));
-  const unsigned chain_wgs = (unsigned)ceil_div(nfiles, 64 * sf::kWavesPerWG);
-  const unsigned grid = chain_wgs + grid_for_blocks((uint64_t)nfiles * nbf);
-  sfi::clear_stale_error();
-  hipLaunchKernelGGL(sf::sha1_staged_kernel<kTile>, dim3(grid), dim3(sf::kThreads), 0, s, base, bs, (uint64_t)nfiles,
-                     nbf, m, flen, dig, nbf, pad, words, chain_wgs, fh, d_status,
-                     chain_spin_limit(), chain_poll_gap());
-  int rc = hip_err(hipGetLastError());
-  (void)hipFreeAsync(words, s);
+  void* state = nullptr;  // every file's SHA-1 state between the two halves of its chain
+  SF_HIP(hipMallocAsync(&state, (size_t)nfiles * 20, s));
+  const sf_chain_job first = {dig, nfiles, 1, nbf, state, nullptr};
+  const sf_chain_job second = {dig, nfiles, 2, nbf, state, fh};
+  int rc = sf_index_device_batch_chained_cols(base, nfiles, flen, bs, 0, cut, dig, nullptr, 0, s);
+  if (rc == SF_OK) rc = sf_index_device_batch_chained_cols(base, nfiles, flen, bs, cut, nbf, dig, &first, 1, s);
+  if (rc == SF_OK) rc = sf_index_device_batch_chained_cols(nullptr, 0, flen, bs, 0, nbf, nullptr, &second, 1, s);
+  (void)hipFreeAsync(state, s);
   return rc;
 }
 
@@ -304,7 +291,7 @@ const char* sf_strerror(int code) {
     case SF_EINVAL: return "invalid argument";
     case SF_ENOSPC: return "output capacity too small";
     case SF_ERANGE: return "block outside the input";
-    case SF_ETIMEDOUT: return "device-side wait timed out (blocks_hash not computed)";
+    case SF_ETIMEDOUT: return "device-side wait timed out (no longer returned)";
     default: return "unknown error";
   }
 }
@@ -394,8 +381,8 @@ static int sf_index_device_batch_body(const void* d_data, uint64_t len, const sf
     const uint8_t* base = static_cast<const uint8_t*>(d_data) + files[0].offset;
     if (!d_file_hashes)
       return launch_fixed(base, total * (uint64_t)block_size, block_size, total, d_digests, s);
-    return batch_staged(base, files[0].len, block_size, n_files, nbf, static_cast<uint8_t*>(d_digests),
-                        static_cast<uint8_t*>(d_file_hashes), d_status, s);
+    return batch_with_hashes(base, files[0].len, block_size, n_files, nbf, static_cast<uint8_t*>(d_digests),
+                             static_cast<uint8_t*>(d_file_hashes), knob(K_BATCH_FUSED) != 0, s);
   }
 
   // Block table for the ragged case, file table for blocks_hash; one device

@@ -393,82 +393,15 @@ __device__ __forceinline__ void sha1_stream_range(Sha1& st, const uint4* __restr
   }
 }
 
-// Coherent read of a counter that waves on every XCD add to: an agent-scope
-// atomic add of a zero the compiler cannot see (hipcc folds an add of a
-// literal 0 into a plain load).  A relaxed agent-scope atomic LOAD is a
-// `global_load ... sc1`: it skips the CU's L1 but is served by the reading
-// XCD's L2, which no other XCD's add invalidates -- once the line is there,
-// the reader sees a frozen count until its own XCD adds again or the line is
-// evicted (tests/test_gpu_robustness.py's XCD litmus shows
-// it).  The read-modify-write is performed where every XCD's adds are.
-__device__ __forceinline__ uint32_t coherent_read_u32(uint32_t* p) {
-  uint32_t zero;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-  return __hip_atomic_fetch_add(p, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Busy-wait about `ticks` of the 100 MHz wall clock (test hook: the delay
-// between a chain lane's polls, SF_TEST_CHAIN_POLL_GAP_US).
-__device__ __forceinline__ void wait_ticks(uint64_t ticks) {
-  const uint64_t t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
-}
-
 // One lane per file: the file's blocks_hash (src/index.rs:661-682) = SHA-1
-// over its run of run_len digest bytes, consumed in S slices of mb bytes (a
-// multiple of 64).  With stage_done, slice k is read only after
-// stage_done[k] == waves_per_stage: ONE lane polls ONE word with a coherent
-// read (coherent_read_u32, s_sleep between polls, at most spin_limit + 1
-// polls), then an agent-scope acquire (MI355X guide, Guideline 16).  A poll
-// that gives up stores an all-zero hash and sets *status = SF_ETIMEDOUT,
-// which the host reads back and returns (the reference never yields a hash it
-// did not compute, src/index.rs:661-682).  Not expected: the producers never
-// wait, the host keeps the chain workgroups below the resident capacity
-// (batch_staged), and the poll sees every XCD's adds; the bound is a backstop.
-// poll_gap (test hook, wall-clock ticks): the wait after a poll that did not
-// match, instead of s_sleep(8).
+// over its run of run_len digest bytes (the stand-alone chain kernel).
 __device__ __forceinline__ void chain_wave(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t f,
-                                           bool valid, uint32_t run_len, uint32_t S, uint32_t mb,
-                                           uint32_t* __restrict__ stage_done, uint32_t waves_per_stage,
-                                           uint8_t* __restrict__ out, int* __restrict__ status,
-                                           uint32_t spin_limit, uint32_t poll_gap) {
-  const int lane = lane_id();
+                                           bool valid, uint32_t run_len, uint8_t* __restrict__ out) {
+  if (!valid) return;
   Sha1 st;
   st.init();
-  const uint8_t* p = runs + (uint64_t)(valid ? f : 0) * run_stride;
-  const uint4* q = reinterpret_cast<const uint4*>(p);
-  bool ok = true;
-  for (uint32_t k = 0; k < S; ++k) {
-    if (stage_done) {
-      uint32_t seen = 0;
-      if (lane == 0) {
-        for (uint32_t spins = 0;; ++spins) {
-          seen = coherent_read_u32(stage_done + k);
-          if (seen >= waves_per_stage || spins >= spin_limit) break;
-          if (poll_gap) wait_ticks(poll_gap);
-          else __builtin_amdgcn_s_sleep(8);
-        }
-      }
-      seen = __builtin_amdgcn_readfirstlane(seen);
-      if (seen < waves_per_stage) {
-        ok = false;
-        if (lane == 0) __hip_atomic_store(status, SF_ETIMEDOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    if (valid) {
-      const uint32_t lo = k * mb, hi = (k + 1 == S) ? (run_len / 64) * 64 : lo + mb;
-      sha1_stream_range(st, q, lo, hi);
-    }
-  }
-  if (!valid) return;
-  if (!ok) {
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + (uint64_t)f * 20);
-    o[0] = o[1] = o[2] = o[3] = o[4] = 0;
-    return;
-  }
+  const uint8_t* p = runs + (uint64_t)f * run_stride;
+  sha1_stream_range(st, reinterpret_cast<const uint4*>(p), 0, (run_len / 64) * 64);
   const uint32_t nch = n_chunks(run_len);
   for (uint32_t c = run_len / 64; c < nch; ++c) {
     uint32_t w[16];
@@ -484,7 +417,7 @@ __global__ void __launch_bounds__(64)
 sha1_chain_kernel(const uint8_t* __restrict__ runs, uint64_t run_stride, uint32_t nfiles, uint32_t run_len,
                   uint8_t* __restrict__ out) {
   const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  chain_wave(runs, run_stride, f, f < nfiles, run_len, 1, run_len, nullptr, 0, out, nullptr, 0, 0);
+  chain_wave(runs, run_stride, f, f < nfiles, run_len, out);
 }
 #endif
 
@@ -567,72 +500,6 @@ __device__ __forceinline__ void chain_job(const ChainJob& j, uint32_t wave, uint
 
 // sha1_fixed_chained_kernel (a stream's batches with their chains) is in
 // sf_stream.hip, its own translation unit.
-
-// Many equal-size files in ONE launch with their blocks_hash chains.
-// `rows` files of `cols` full-size blocks.  Workgroups [0, chain_wgs) are
-// chain workgroups: each wave owns 64 files and runs chain_wave over S
-// stages.  The others hash blocks: stage k = columns [k*m, (k+1)*m) of every
-// file, numbered stage-major (stage, row, column) so the dispatcher finishes
-// stage k roughly before stage k+1; block (row, col) reads
-// data[row*in_stride + col*bs, +bs) and writes out[row*out_stride + col].
-// After storing its 64 digests each block wave publishes one arrival on
-// stage_done[stage] (drain, agent release, drain, relaxed agent add).
-// Deadlock-free by construction: only chain waves wait, and only on block
-// waves, which never wait; the bounded poll is a backstop.
-// rows*m must be a multiple of 64 (no wave straddles two stages).
-constexpr int kStagedWavesPerSimd = 4;  // min waves/SIMD of the staged kernel
-template <int TILE>
-__global__ void __launch_bounds__(kThreads, kStagedWavesPerSimd)
-sha1_staged_kernel(const uint8_t* __restrict__ data, uint32_t bs, uint64_t rows, uint64_t cols, uint64_t m,
-                   uint64_t in_stride, uint8_t* __restrict__ digests, uint64_t out_stride, const PadSchedule pad,
-                   uint32_t* __restrict__ stage_done, uint32_t chain_wgs, uint8_t* __restrict__ file_hashes,
-                   int* __restrict__ status, uint32_t spin_limit, uint32_t poll_gap) {
-  __shared__ uint4 smem[kWavesPerWG * 64 * (TILE / 16)];
-  const int lane = lane_id();
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t per_stage = rows * m;
-  if (blockIdx.x < chain_wgs) {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound chains issue first on a shared SIMD
-    const uint32_t f = (blockIdx.x * kWavesPerWG + wid) * 64 + lane;
-    chain_wave(digests, out_stride * 20, f, f < rows, (uint32_t)(cols * 20), (uint32_t)(cols / m),
-               (uint32_t)(m * 20), stage_done, (uint32_t)(per_stage / 64), file_hashes, status, spin_limit,
-               poll_gap);
-    return;
-  }
-  const uint64_t nblocks = rows * cols;
-  const uint64_t first = ((uint64_t)(blockIdx.x - chain_wgs) * kWavesPerWG + wid) * 64;
-  if (first >= nblocks) return;
-  const uint64_t stage = first / per_stage;  // wave-uniform
-  const uint64_t blk = first + lane;
-  const bool valid = blk < nblocks;
-  const uint64_t w = (valid ? blk : first) - stage * per_stage;
-  const uint64_t row = w / m, col = stage * m + (w - (w / m) * m);
-  const uint64_t off = row * in_stride + col * bs;
-  const uint64_t w0 = first - stage * per_stage;
-  const uint64_t wl = (first + 64 <= nblocks ? first + 63 : nblocks - 1) - stage * per_stage;
-  WaveGeo geo;
-  geo.base = (w0 / m) * in_stride + (stage * m + w0 % m) * bs;
-  geo.span = (wl / m) * in_stride + (stage * m + wl % m) * bs + bs - geo.base;
-  geo.min_size = bs;
-  geo.max_size = bs;
-  geo.max_nch = n_chunks(bs);
-  geo.lds_ok = ((bs & 15u) == 0) && ((in_stride & 15u) == 0) && ((reinterpret_cast<uintptr_t>(data) & 15u) == 0) &&
-               geo.span < 0xF0000000ull;
-  const uint32_t rel = (uint32_t)(off - geo.base);
-  Sha1 st;
-  Adler wk;  // unused (no weak sum in the staged batch)
-  hash_wave<TILE, true>(data, off, valid ? bs : 0u, rel, valid, geo, smem + wid * 64 * (TILE / 16), st, pad, wk);
-  if (chain_wgs == 0 && file_hashes == nullptr) {  // experiment: blocks only, no publish
-    if (valid) st.store(digests + (row * out_stride + col) * 20);
-    return;
-  }
-  // Publish (MI355X guide, hand-off flag form): write-through (sc1) digest
-  // stores, drained by this wave, then one relaxed agent-scope add.  No
-  // agent release fence: a per-wave L2 write-back cost ~0.95 ms per 8 GiB.
-  if (valid) st.store_writethrough(digests + (row * out_stride + col) * 20);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(stage_done + stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ------------------------------------------- explicit lists at any offset
 // The reference's default blocks are content-defined (cdchunking ZPAQ,

@@ -1,15 +1,15 @@
 // sf_litmus.hip -- test hook sf_test_xcd_litmus (include/syncfast_amd_test.h):
-// the cross-XCD counter read that the fused many-file launch's blocks_hash
-// lanes depend on (sha1_staged_kernel, sf_kernels.hpp chain_wave), in
+// the cross-XCD counter read that round 5's fused many-file launch's
+// blocks_hash lanes polled (sha1_staged_kernel, removed in round 6), in
 // isolation.  Its own translation unit, so it cannot change how the product
 // kernels compile.
 //
 // One launch of kLitmusWGs one-wave workgroups, lane 0 of each doing the work:
 //   * workgroup 0 (the reader) reads the counter once with the form under
 //     test -- mode 0: a relaxed agent-scope atomic load (`global_load ... sc1`,
-//     the poll the fused launch used until round 6); mode 1: an agent-scope
-//     atomic add of an opaque zero (the poll it uses now) -- which puts the
-//     counter's line in its XCD's L2 for mode 0, then publishes its XCD id;
+//     round 5's poll); mode 1: an agent-scope atomic add of an opaque zero
+//     -- which puts the counter's line in its XCD's L2 for mode 0 if loads
+//     allocate there, then publishes its XCD id;
 //   * every other workgroup on ANOTHER XCD adds 1 to the counter once the
 //     reader says go; workgroups on the reader's XCD never touch the counter's
 //     line (a same-XCD atomic would drop it from that L2);

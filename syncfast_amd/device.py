@@ -181,13 +181,11 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
     ``files`` = [(offset, length), ...].  Returns (digests uint8[n,20],
     first_block int64[n_files+1], file_hashes uint8[n_files,20] or None).
 
-    The per-file blocks_hash lanes of an equal-size batch wait (bounded) for
-    the digests they consume; a wait that gives up is reported as
-    SF_ETIMEDOUT.  With ``status`` (int32[1] on the device, zeroed by the
-    caller) the call stays asynchronous and the caller checks it; without,
-    the call synchronises the stream and raises SfError(SF_ETIMEDOUT).  The
-    bound is a backstop: the lanes poll with a coherent read (DESIGN.md 3.3;
-    the one time it ran out, round 5, the poll was an L2-served load)."""
+    An equal-size batch with file_hashes runs ONE fused launch in which no
+    wave waits (the chains' slices run on the waves that complete their
+    dependencies), so nothing can time out.  ``status``
+    (int32[1] on the device, may be None) is passed through and is never
+    written; it stays for callers of the round-5 interface."""
     _require_device(data, "data", torch.uint8)
     nf = len(files)
     descs = (FileDesc * max(nf, 1))()
@@ -212,10 +210,7 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
                 raise ValueError("hashes_out too small")
         first = np.zeros(nf + 1, np.uint64)
         nb = ctypes.c_uint64(0)
-        own_status = status is None and fh is not None
-        if own_status:
-            status = torch.zeros(1, dtype=torch.int32, device=data.device)
-        elif status is not None:
+        if status is not None:
             _require_device(status, "status", torch.int32, data.device)
         check(lib().sf_index_device_batch(data.data_ptr() if data.numel() else None, data.numel(), descs, nf,
                                           block_size, dig.data_ptr() if total else None, dig.numel() // 20,
@@ -224,10 +219,6 @@ def index_device_batch(data: torch.Tensor, files: Sequence[Tuple[int, int]], blo
                                           status.data_ptr() if status is not None else None,
                                           _stream_ptr(data, stream)),
               "sf_index_device_batch")
-        if own_status:
-            code = int(status.item())
-            if code != 0:  # SF_ETIMEDOUT: a blocks_hash lane gave up; its hash was not computed
-                raise SfError(code, "sf_index_device_batch")
     return dig, first.astype(np.int64), fh
 
 

@@ -95,12 +95,12 @@ def test_knobs_latched_at_load_and_set_by_the_hook(monkeypatch):
         assert old == before and _lib.get_knob("SF_TEST_TABLE_SORT") == 1
     finally:
         _lib.set_knob("SF_TEST_TABLE_SORT", before)
-    for gone in ("SF_TABLE_SORT", "SF_CHAIN_SPIN_LIMIT", "SF_LAUNCH_MAX_BLOCKS", "SF_INPLACE_FAIL_AT", "SF_STAGES",
+    for gone in ("SF_TEST_CHAIN_SPIN_LIMIT", "SF_TEST_CHAIN_POLL_GAP_US", "SF_TEST_STAGES", "SF_TABLE_SORT", "SF_CHAIN_SPIN_LIMIT", "SF_LAUNCH_MAX_BLOCKS", "SF_INPLACE_FAIL_AT", "SF_STAGES",
                  "SF_FILE_INPLACE", "SF_MAP_MIN_MIB"):
         with pytest.raises(_lib.SfError):
             _lib.get_knob(gone)
-    for name in ("SF_TEST_CHAIN_SPIN_LIMIT", "SF_TEST_LAUNCH_MAX_BLOCKS", "SF_TEST_INPLACE_FAIL_AT",
-                 "SF_TEST_STAGES", "SF_TEST_WIRE_CHUNK", "SF_TEST_STREAM_STAGE_MIB", "SF_IO_THREADS"):
+    for name in ("SF_BATCH_FUSED", "SF_TEST_LAUNCH_MAX_BLOCKS", "SF_TEST_INPLACE_FAIL_AT",
+                 "SF_TEST_WIRE_CHUNK", "SF_TEST_STREAM_STAGE_MIB", "SF_IO_THREADS"):
         _lib.get_knob(name)
     assert _lib.get_stat("pages_locked") >= 0 and _lib.get_stat("not_anon_refused") >= 0
 

@@ -1,20 +1,18 @@
 """GPU: failure paths of the C-ABI report errors instead of wrong results.
 
-- The fused many-file launch (sha1_staged_kernel): its blocks_hash lanes wait
-  (bounded) for block digests; a wait that gives up must surface as
-  SF_ETIMEDOUT in the caller's status word (or SfError from the Python
-  wrapper), never as an all-zero blocks_hash with rc = 0 (the reference never
-  yields a hash it did not compute, src/index.rs:661-682); sf_index_files
-  never takes the waiting path.  Forced with SF_TEST_CHAIN_SPIN_LIMIT=0 (one
-  poll per wait; test hook).
-- The lanes' poll sees every XCD's arrivals: a lane whose first poll comes
-  before the block waves finish and whose next comes after they all have
-  (SF_TEST_CHAIN_POLL_GAP_US) completes at the default bound, and the XCD
-  litmus (sf_test_xcd_litmus) shows the poll's read-modify-write seeing adds
-  made on other XCDs after its XCD's L2 holds the line.
-- Batches too wide for the fused launch's chain workgroups to stay below the
-  resident capacity, and callers without a status word, take the non-waiting
-  path: correct hashes even with the spin limit at 0.
+- Equal-size batches with every file's blocks_hash (sf_index_device_batch):
+  since round 6 no wave waits for another -- the batch is hashed in two
+  column halves with the first half of the chains beside the second half's
+  blocks, then the second half of the chains alone (the batch stream's last
+  batch) -- so there is no bound to give up at and no SF_ETIMEDOUT (its one
+  occurrence, round 5, came from the single fused launch whose chain lanes
+  polled stage counters).  Checked for ragged file groups, 70,000 files,
+  under uneven load (a long kernel on another stream of the device), two
+  streams of batches, the blocks-then-chains form (SF_BATCH_FUSED=0) and
+  unaligned outputs; a status word passed in is never written.
+- The XCD litmus (sf_test_xcd_litmus): a counter read after other XCDs'
+  adds, by a relaxed agent-scope atomic load and by an atomic add of an
+  opaque zero.
 - A file truncated while indexed (default pread route): no hang or SIGBUS,
   an error or a complete result.
 - index_file sized from a stale stat retries with the need (SF_ENOSPC)."""
@@ -28,7 +26,7 @@ import torch
 
 import oracle
 from syncfast_amd import device, host
-from syncfast_amd._lib import SF_ETIMEDOUT, FileDesc, SfError, lib
+from syncfast_amd._lib import FileDesc, SfError, lib
 
 pytestmark = pytest.mark.gpu
 
@@ -40,38 +38,66 @@ def _equal_batch(gpu, nfiles, nbf, bs, seed):
     return data, t, files
 
 
-def test_staged_chain_timeout_is_reported(gpu, knobs):
-    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
-    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 501)  # 256 MiB: stage 0 cannot be done at the first poll
-    # the asynchronous form: the caller's status word carries it
-    st = torch.zeros(1, dtype=torch.int32, device=gpu)
-    device.index_device_batch(t, files, 4096, status=st)
-    assert int(st.item()) == SF_ETIMEDOUT
-    # without one, the wrapper raises: no hash it did not compute, no rerun
-    with pytest.raises(SfError) as e:
-        device.index_device_batch(t, files, 4096)
-    assert e.value.code == SF_ETIMEDOUT
-
-
-@pytest.mark.parametrize("gap_us", [50_000, 20])
-def test_staged_poll_after_every_block_wave_finished(gpu, knobs, gap_us):
-    # A lane's first poll of stage 0 comes right at the launch's start (the
-    # chain workgroups are dispatched first), before the stage is done; with a
-    # 50 ms gap its next poll comes after every block wave of the 256 MiB
-    # launch has finished, when no XCD adds to the counters any more (the
-    # window in which an L2-served load of the counter line stays stale);
-    # with 20 us it polls many times while they run.  The default bound
-    # holds either way and every blocks_hash is the oracle's.
-    knobs.set("SF_TEST_CHAIN_POLL_GAP_US", gap_us)
-    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 508)
-    st = torch.zeros(1, dtype=torch.int32, device=gpu)
-    dig, _, fh = device.index_device_batch(t, files, 4096, status=st)
-    assert int(st.item()) == 0
-    want = oracle.index_fixed_mt(data, 4096, 8)
+def _check_batch(data, nfiles, nbf, bs, dig, fh, every=1):
+    want = oracle.index_fixed_mt(data, bs, 8)
     assert np.array_equal(dig.cpu().numpy(), want)
     fhn = fh.cpu().numpy()
-    for i in range(64):
-        assert bytes(fhn[i]) == oracle.blocks_hash(want[i * 1024:(i + 1) * 1024]), i
+    for i in list(range(0, nfiles, every)) + [nfiles - 1]:
+        assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
+
+
+@pytest.mark.parametrize("nbf", [64, 128, 1024, 2048, 1028])
+@pytest.mark.parametrize("nfiles", [1, 63, 64, 65, 130])
+def test_batch_halves_every_shape(gpu, nbf, nfiles):
+    # files of 64 .. 2048 blocks (64: one column wave, no halves; 1028: not
+    # a multiple of 64, blocks then chains) and ragged last chain waves (files
+    # not a multiple of 64); the status word passed in is never written
+    bs = 1024
+    data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 500 + nbf + nfiles)
+    st = torch.full((1,), 7, dtype=torch.int32, device=gpu)
+    dig, _, fh = device.index_device_batch(t, files, bs, status=st)
+    assert int(st.item()) == 7
+    _check_batch(data, nfiles, nbf, bs, dig, fh)
+
+
+def test_staged_under_uneven_load(gpu):
+    # a long kernel on another stream of the device holds most of the CUs
+    # while fused launches run: the waves of a launch complete in an order
+    # far from the dispatch order, and no wave waits for another anyway
+    big = device.splitmix_tensor(8 << 30, 9, device=gpu)
+    side = torch.cuda.Stream(gpu)
+    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 502)
+    torch.cuda.synchronize(gpu)
+    outs = []
+    for r in range(4):
+        device.index_device(big, 4096, stream=side)  # ~2.4 ms beside the launches below
+        dig = torch.empty((64 * 1024, 20), dtype=torch.uint8, device=gpu)
+        fh = torch.empty((64, 20), dtype=torch.uint8, device=gpu)
+        device.index_device_batch(t, files, 4096, out=dig, hashes_out=fh)
+        outs.append((dig, fh))
+    torch.cuda.synchronize(gpu)
+    for dig, fh in outs:
+        _check_batch(data, 64, 1024, 4096, dig, fh)
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+def test_staged_two_streams(gpu, knobs, fused):
+    # fused launches alternating on two streams with nothing between them
+    # (sf_index_files' pattern), and the same with SF_BATCH_FUSED=0
+    knobs.set("SF_BATCH_FUSED", fused)
+    data, t, files = _equal_batch(gpu, 32, 2048, 4096, 503)
+    ss = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+    outs = []
+    for i in range(40):
+        s = ss[i & 1]
+        with torch.cuda.stream(s):
+            dig = torch.empty((32 * 2048, 20), dtype=torch.uint8, device=gpu)
+            fh = torch.empty((32, 20), dtype=torch.uint8, device=gpu)
+            device.index_device_batch(t, files, 4096, out=dig, hashes_out=fh, stream=s)
+            outs.append((dig, fh))
+    torch.cuda.synchronize(gpu)
+    for dig, fh in outs[:2] + outs[-2:]:
+        _check_batch(data, 32, 2048, 4096, dig, fh, every=7)
 
 
 def test_xcd_counter_litmus(gpu):
@@ -92,40 +118,22 @@ def test_xcd_counter_litmus(gpu):
         print(f"litmus mode {mode}: reader XCD {xcc}, {adders} adds from other XCDs, second read {v1}")
 
 
-def test_staged_default_spin_limit_is_green(gpu):
-    data, t, files = _equal_batch(gpu, 64, 1024, 4096, 502)
-    st = torch.zeros(1, dtype=torch.int32, device=gpu)
-    dig, _, fh = device.index_device_batch(t, files, 4096, status=st)
-    assert int(st.item()) == 0
-    want = oracle.index_fixed_mt(data, 4096, 8)
-    assert np.array_equal(dig.cpu().numpy(), want)
-    assert bytes(fh.cpu().numpy()[63]) == oracle.blocks_hash(want[63 * 1024:])
-
-
-def test_index_files_never_waits(gpu, tmp_path, knobs):
-    # sf_index_files hashes each stage on the batch path that never waits
-    # (no status word: block kernel, then chain kernel), so a zero spin limit
-    # changes nothing: every blocks_hash equals the oracle's
+def test_index_files_blocks_hash(gpu, tmp_path):
+    # sf_index_files: every stage's blocks and blocks_hash chains through
+    # sf_index_device_batch; every blocks_hash equals the oracle's
     paths = []
     for i in range(32):
         p = tmp_path / f"f{i}"
         p.write_bytes(oracle.splitmix_bytes(8 << 20, 600 + i).tobytes())
         paths.append(str(p))
-    rows, first, fh = host.index_files(paths, 4096)  # green first
-    want = oracle.index_fixed(np.fromfile(paths[5], np.uint8), 4096)[2]
-    assert bytes(fh[5]) == oracle.blocks_hash(want)
-    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
-    rows2, first2, fh2 = host.index_files(paths, 4096)
-    assert np.array_equal(rows2, rows) and np.array_equal(first2, first) and np.array_equal(fh2, fh)
+    rows, first, fh = host.index_files(paths, 4096)
     for i in (0, 5, 31):
         w = oracle.index_fixed(np.fromfile(paths[i], np.uint8), 4096)[2]
-        assert bytes(fh2[i]) == oracle.blocks_hash(w), i
+        assert bytes(fh[i]) == oracle.blocks_hash(w), i
 
 
-def test_null_status_takes_nonwaiting_path(gpu, knobs):
-    # no status word: the batch runs block kernel + chain kernel (no waits),
-    # so even a zero spin limit gives the right hashes
-    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
+def test_null_status_raw_call(gpu):
+    # the raw C-ABI call with no status word: the same fused launch
     nfiles, nbf, bs = 64, 1024, 4096
     data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 503)
     descs = (FileDesc * nfiles)(*[FileDesc(o, ln) for o, ln in files])
@@ -136,26 +144,31 @@ def test_null_status_takes_nonwaiting_path(gpu, knobs):
                                      fh.data_ptr(), None, ctypes.byref(nb), None,
                                      torch.cuda.current_stream().cuda_stream)
     assert rc == 0
-    want = oracle.index_fixed_mt(data, bs, 8)
-    fhn = fh.cpu().numpy()
-    assert np.array_equal(dig.cpu().numpy(), want)
-    for i in (0, 31, 63):
-        assert bytes(fhn[i]) == oracle.blocks_hash(want[i * nbf:(i + 1) * nbf]), i
+    _check_batch(data, nfiles, nbf, bs, dig, fh, every=31)
 
 
-def test_wide_batch_keeps_chains_below_residency(gpu, knobs):
-    # 70,000 equal files: more chain workgroups (274) than CUs (256) -> the
-    # non-waiting path; with the spin limit at 0 a fused launch would time out
-    knobs.set("SF_TEST_CHAIN_SPIN_LIMIT", 0)
+def test_wide_batch(gpu):
+    # 70,000 equal files, 1094 file groups x 2 stages of chain slices
     nfiles, nbf, bs = 70_000, 128, 64
     data, t, files = _equal_batch(gpu, nfiles, nbf, bs, 504)
     dig, _, fh = device.index_device_batch(t, files, bs)
-    want = oracle.index_fixed_mt(data, bs, 8)
-    assert np.array_equal(dig.cpu().numpy(), want)
-    fhn = fh.cpu().numpy()
-    per = want.reshape(nfiles, nbf, 20)
-    for i in list(range(0, nfiles, 997)) + [nfiles - 1]:
-        assert bytes(fhn[i]) == oracle.blocks_hash(per[i]), i
+    _check_batch(data, nfiles, nbf, bs, dig, fh, every=997)
+
+
+def test_unaligned_outputs(gpu):
+    # a hashes_out 20 B into a larger tensor (any alignment is fine for the
+    # hashes) and a digest table 4 B off a 16-B boundary (file runs not 16-B
+    # aligned: blocks then the per-lane chain kernel); same hashes
+    data, t, files = _equal_batch(gpu, 70, 1024, 4096, 505)
+    buf = torch.empty((71, 20), dtype=torch.uint8, device=gpu)
+    fh = buf[1:]
+    dig, _, _ = device.index_device_batch(t, files, 4096, hashes_out=fh)
+    _check_batch(data, 70, 1024, 4096, dig, fh, every=13)
+    big = torch.empty(70 * 1024 * 20 + 4, dtype=torch.uint8, device=gpu)
+    dig2 = big[4:].view(70 * 1024, 20)
+    fh2 = torch.empty((70, 20), dtype=torch.uint8, device=gpu)
+    device.index_device_batch(t, files, 4096, out=dig2, hashes_out=fh2)
+    _check_batch(data, 70, 1024, 4096, dig2, fh2, every=13)
 
 
 def test_truncated_while_indexed_no_hang(gpu, tmp_path):
