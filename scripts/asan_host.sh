@@ -55,6 +55,8 @@ run zpaq_par -Z -p 4 "$W"/f0* || rc=1  # the file cut on 4 threads, read once, h
 run zpaq_par2 -Z -p 4 -W "$W"/f0* || rc=1  # sf_cut_fd, then sf_index_fd_blocks
 run zpaq_many -Z -M -j 4 -S 1 -P 2 "$W"/f0* || rc=1
 run zpaq_many_small -Z -M -j 4 -S 1 "$W"/s* || rc=1
+run zpaq_many_large -Z -M -j 4 -S 1 -K 1 "$W"/f0* "$W"/s00* || rc=1  # files >= 1 MiB alone through sf_index_fd_cut, in walk order
+SF_TEST_CUT_WINDOW_MIB=1 run zpaq_par_win -Z -p 4 "$W"/f0* || rc=1  # 1 MiB windows: double-buffered window seams
 run multi -X 0 -b 4096 "$W"/f0* || rc=1  # one file on every visible device from one process
 run wire_cdc -v 20000001 || rc=1
 # every route over the same files gives the same rows and blocks_hash
