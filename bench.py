@@ -211,10 +211,11 @@ def config_block(a, world):
                 "rotating" if a.gather_root == "rotate" else "0") if gather else "")}
 
 
-def check_launch(a, world, rank) -> None:
+def check_launch(a, world, rank, fallback_note=None) -> None:
     """CPU-only rehearsal of the N-rank launch (gloo): every rank joins, the
     world size is checked, and rank 0 prints the `multi` block built from
-    stand-in per-rank numbers (the kernel is not run without a GPU)."""
+    stand-in per-rank numbers (the kernel is not run without a GPU) and, after
+    a failed library path, the `multi_fallback` note a real line would carry."""
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=a.dist_timeout))
@@ -225,8 +226,11 @@ def check_launch(a, world, rank) -> None:
     multi = multi_block(dist, torch, torch.device("cpu"), a, rank, world, float(rank + 1), [0.0] * a.steps, roots,
                         "gloo")
     if rank == 0:
-        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item()),
-                          "config": config_block(a, world), "multi": multi}), flush=True)
+        line = {"launch_check": True, "n_gpus": dist.get_world_size(), "ranks_seen": int(seen.item()),
+                "config": config_block(a, world), "multi": multi}
+        if fallback_note:
+            line["multi_fallback"] = fallback_note
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 
 
@@ -801,7 +805,9 @@ def library_main(a, n=None):
     plan = library_plan(a, n)
     ndev = torch.cuda.device_count()
     if ndev < n:
-        raise SystemExit(f"--gpus {n}: only {ndev} device(s) visible")
+        # RuntimeError, not SystemExit: under the driver's torchrun a rank may
+        # see only its own GPU, and the caller then falls back to the per-process form
+        raise RuntimeError(f"--gpus {n}: only {ndev} device(s) visible to one process")
     bs, total = plan["block_size"], plan["total_bytes"]
     nb_total = plan["blocks"]
     L = _lib.lib()
@@ -1032,10 +1038,13 @@ def torchrun_library(a):
     if rank == 0:
         try:
             library_main(a)
-        except Exception as e:  # noqa: BLE001 -- the per-process form measures instead
-            err = f"{type(e).__name__}: {e}"[:500]
+        except (Exception, SystemExit) as e:  # noqa: BLE001 -- the per-process form measures instead
+            err = f"{type(e).__name__}: {e}"[:500] or "failed"
             print(f"bench.py: library multi-GPU path failed ({err}); every rank runs the per-process form",
                   file=sys.stderr, flush=True)
+        if err:  # the failed path's tensors are unreferenced once its frames are gone
+            import gc
+            gc.collect()
             torch.cuda.empty_cache()
     box = [err]
     dist.broadcast_object_list(box, src=0)
@@ -1069,7 +1078,7 @@ def main():
             return torchrun_library(a)
         try:
             return library_main(a)
-        except Exception as e:  # noqa: BLE001 -- reported, then the per-process form measures instead
+        except (Exception, SystemExit) as e:  # noqa: BLE001 -- reported, then the per-process form measures instead
             if a.gpus == 1:
                 raise
             msg = f"{type(e).__name__}: {e}"
@@ -1094,7 +1103,7 @@ def torch_main(a, fallback_note=None):
     if a.events == "auto":
         a.events = "region" if world == 1 else "step"
     if a.check_launch:
-        return check_launch(a, world, rank)
+        return check_launch(a, world, rank, fallback_note)
 
     import torch
     import torch.distributed as dist

@@ -159,3 +159,26 @@ def test_multi_path_resolution():
     assert ns(gpus=2, dist_backend="gloo").multi_path == "torch"
     assert ns(gpus=8, multi_path="torch").multi_path == "torch"
     assert ns(gpus=8, config=2).config == 2
+
+
+def test_torchrun_library_failure_falls_back_on_every_rank():
+    """The driver's torchrun with the library path: rank 0 drives every device
+    in one process and the other ranks wait.  If rank 0's path fails for any
+    reason -- here: no GPU, so fewer devices than --gpus, as when a launcher
+    shows each rank only its own GPU -- every rank must go on to the
+    per-process form (here its launch rehearsal) and the line must say why,
+    never leave the other ranks waiting."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "2",
+                        "--multi-path", "library", "--check-launch", "--dist-timeout", "60"],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["launch_check"] and line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    assert "RuntimeError" in line["multi_fallback"] and "device(s) visible" in line["multi_fallback"]
+    assert "library multi-GPU path failed" in r.stderr
