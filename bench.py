@@ -138,6 +138,9 @@ def parse():
                    help="library path: GiB per device of the e2e_file_multi leg (a file on disk through "
                         "sf_index_file_multi; 0 = skip)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal only)")
+    p.add_argument("--library-timeout", type=float, default=900.0,
+                   help="library path: seconds before a call that never returns (a stuck RCCL exchange) ends "
+                        "the process with an error instead of hanging the run")
     p.add_argument("--dist-timeout", type=float, default=300.0,
                    help="seconds before a stuck collective fails the run (init_process_group timeout)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -798,11 +801,28 @@ def library_main(a, n=None):
     before a table is reused).  value = n x shard bytes x steps / wall time
     of the timed steps (every device synchronised on both sides).  Kernel time
     from HIP events on each device's hash stream around its launch."""
+    import threading
+    n = a.gpus if n is None else n
+    plan = library_plan(a, n)
+
+    def stuck():  # a hang inside the library (RCCL) cannot be interrupted: end the process loudly
+        print(f"bench.py: library multi-GPU path still running after {a.library_timeout:.0f} s; exiting",
+              file=sys.stderr, flush=True)
+        os._exit(3)
+
+    watchdog = threading.Timer(a.library_timeout, stuck)
+    watchdog.daemon = True
+    watchdog.start()
+    try:
+        return _library_run(a, n, plan)
+    finally:
+        watchdog.cancel()
+
+
+def _library_run(a, n, plan):
     import torch
     import numpy as np
     from syncfast_amd import _lib, device, host
-    n = a.gpus if n is None else n
-    plan = library_plan(a, n)
     ndev = torch.cuda.device_count()
     if ndev < n:
         # RuntimeError, not SystemExit: under the driver's torchrun a rank may
