@@ -765,7 +765,7 @@ def library_plan(a, n):
     without a GPU (--check-plan; tests/test_bench_launch.py): one logical file
     of n shards (configs[3]: n x 32 GiB at 4 KiB blocks), shard r on device r
     (sf_shard_range = syncfast_amd.shard.shard_range), three rotating scratch
-    tables per device, one receive table per device (the gather's root
+    tables per device, two receive tables per device, used in turn (the gather's root
     rotates: step i of the timed steps goes to device (i - (steps-1)) mod n,
     so the last timed step's table is device 0's), and the rows of each
     device's shard in the root's table (sf_test_multi_plan's offsets)."""
@@ -785,7 +785,7 @@ def library_plan(a, n):
     roots_timed = [(i - (a.steps - 1)) % n for i in range(a.steps)]
     return {"path": "library", "n_devices": n, "config": a.config, "workload": cfg["workload"], "block_size": bs,
             "bytes_per_gpu": per, "total_bytes": total, "blocks": total // bs, "shards": shards,
-            "scratch_tables_per_device": 3, "receive_table_rows": total // bs,
+            "scratch_tables_per_device": 3, "receive_tables_per_device": 2, "receive_table_rows": total // bs,
             "roots_warmup": list(range(n)), "roots_timed": roots_timed,
             "entry": "sf_index_device_multi_ex (hash streams + gather streams)"}
 
@@ -797,8 +797,8 @@ def library_main(a, n=None):
     device r on its hash stream (sha1_fixed_kernel) and, on the gather
     streams, sends every other shard's table to the step's root (rotating),
     inside the library; the next step's hashing overlaps the previous step's
-    exchange (three scratch tables per device, events on the gather streams
-    before a table is reused).  value = n x shard bytes x steps / wall time
+    exchange (three scratch tables and two receive tables per device, events
+    on the gather streams before a table is reused).  value = n x shard bytes x steps / wall time
     of the timed steps (every device synchronised on both sides).  Kernel time
     from HIP events on each device's hash stream around its launch."""
     import threading
@@ -839,7 +839,7 @@ def _library_run(a, n, plan):
             device.fill_splitmix(t, SEED, sh["start"])
             data.append(t)
             digs.append([torch.empty((max(sh["rows"], 1), 20), dtype=torch.uint8, device=devs[r]) for _ in range(3)])
-            tables.append(torch.empty((max(nb_total, 1), 20), dtype=torch.uint8, device=devs[r]))
+            tables.append([torch.empty((max(nb_total, 1), 20), dtype=torch.uint8, device=devs[r]) for _ in range(2)])
             hs.append(torch.cuda.Stream(devs[r]))
             gs.append(torch.cuda.Stream(devs[r]))
     for r in range(n):
@@ -849,7 +849,13 @@ def _library_run(a, n, plan):
     hs_p, gs_p = vp([s.cuda_stream for s in hs]), vp([s.cuda_stream for s in gs])
     scratch_p = [vp([digs[r][b].data_ptr() for r in range(n)]) for b in range(3)]
     send_ev = [[None] * 3 for _ in range(n)]  # gather stream r past the exchange that read digs[r][b]
-    table_ev = [None] * n  # gather stream r past the last exchange into tables[r]
+    # gather stream r past the last exchange into tables[r][k]: a root's next
+    # step hashes into its other table, so it never waits for the exchange
+    # just issued (with one table, N = 1 serialised every exchange behind the
+    # next step's hashing)
+    table_ev = [[None, None] for _ in range(n)]
+    uses = [0] * n  # steps each device has been root for (its tables in turn)
+    last = [None]  # (root, table) of the last step
     self_gather = n == 1 and _lib.get_knob("SF_TEST_MULTI_SELF_GATHER") != 0
     exchange = n > 1 or self_gather  # else the library only hashes (the table is whole on hs[0])
     kern = [[] for _ in range(n)]  # (e0, e1) per timed step on each hash stream
@@ -860,15 +866,18 @@ def _library_run(a, n, plan):
         for r in range(n):
             if send_ev[r][b] is not None:
                 hs[r].wait_event(send_ev[r][b])
-        if table_ev[root] is not None:
-            hs[root].wait_event(table_ev[root])
+        k = uses[root] % 2
+        uses[root] += 1
+        last[0] = (root, k)
+        if table_ev[root][k] is not None:
+            hs[root].wait_event(table_ev[root][k])
         evs = []
         if timed:
             for r in range(n):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(hs[r])
                 evs.append(e0)
-        _lib.check(L.sf_index_device_multi_ex(n, shard_p, total, bs, scratch_p[b], root, tables[root].data_ptr(),
+        _lib.check(L.sf_index_device_multi_ex(n, shard_p, total, bs, scratch_p[b], root, tables[root][k].data_ptr(),
                                               hs_p, gs_p), "sf_index_device_multi_ex")
         if timed:
             for r in range(n):
@@ -880,7 +889,7 @@ def _library_run(a, n, plan):
             e.record(gs[r])
             send_ev[r][b] = e
             if r == root:
-                table_ev[r] = e
+                table_ev[r][k] = e
                 if timed and exchange:
                     gather_ev.append((root, kern[root][-1][1], e))
 
@@ -914,7 +923,8 @@ def _library_run(a, n, plan):
     # first and last block (product host SHA-1) and, for the other devices,
     # against their scratch table of that step
     b_last = (a.steps - 1) % 3
-    tab = tables[roots[-1]][:nb_total]
+    assert last[0][0] == roots[-1]
+    tab = tables[last[0][0]][last[0][1]][:nb_total]
     for r, sh in enumerate(plan["shards"]):
         if not sh["rows"]:
             continue
