@@ -108,18 +108,24 @@ inline unsigned device_cus() {
   return (unsigned)v;
 }
 
-// Explicit block lists of at least this many blocks are hashed in order of
+// Explicit block lists of at least two waves' blocks are hashed in order of
 // length (sha1_table_kernel's `order`): a wave runs as long as its longest
 // block, so 64 blocks of mixed sizes side by side waste most lanes -- a list
 // of content-defined sizes (mean 8 KiB, up to 32 KiB) hashed at 312 GiB/s in
-// list order against 1834 GiB/s sorted (scripts/ragged_probe.py).  Below a
-// few waves per wave slot the sort cannot shorten the launch (every wave is
-// resident at once and the longest block sets the time), so small lists keep
-// their order.  SF_TEST_TABLE_SORT=0 / 1 never / always sorts (test hook).
+// list order against 1834 GiB/s sorted (scripts/ragged_probe.py).  Small
+// lists too (round 6; until then only from 2^17 blocks, on the reasoning that
+// with every wave resident at once the longest block sets the time either
+// way): a mixed wave also runs every step in the slot path's per-lane tail
+// loop, its shortest block ending the branch-free steps, one compression at a
+// time; sorted, the wave holding the longest blocks runs them two at a time.
+// configs[0]'s one-window list (8,415 blocks): the kernel 1.28 -> 0.69 ms,
+// the sort's three kernels 19 us (profiles/r06/sort_small/).  One wave has
+// nothing to reorder.  SF_TEST_TABLE_SORT=0 / 1 never / always sorts (test hook).
+constexpr uint64_t kTableSortMinBlocks = 128;
 inline uint64_t table_sort_min() {
   const int64_t v = knob(K_TEST_TABLE_SORT);
   if (v >= 0) return v ? 1 : ~0ull;
-  return 1ull << 17;
+  return kTableSortMinBlocks;
 }
 constexpr uint64_t kSortMaxBlocks = 1ull << 27;  // blocks per sorted piece (~1.2 GiB of workspace at most)
 
@@ -149,14 +155,14 @@ uint32_t* table_order(const uint32_t* d_sizes, uint64_t n, hipStream_t s, void**
   // one counting pass over 256 / 512 / 1024 classes (sf_sort.hip)
   const size_t ob = up(n * 4), total = ob + up(sfi::class_order_workspace(n, kmax));
   uint8_t* ws = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&ws), total, s) != hipSuccess) {
+  if (sfi::stream_alloc(reinterpret_cast<void**>(&ws), total, s) != SF_OK) {
     (void)hipGetLastError();
     return nullptr;
   }
   uint32_t* order = reinterpret_cast<uint32_t*>(ws);
   if (sfi::class_order(d_sizes, n, mbits, kmax, ws + ob, order, s) != SF_OK) {
     (void)hipGetLastError();
-    (void)hipFreeAsync(ws, s);
+    sfi::stream_free(ws, s);
     return nullptr;
   }
   *ws_out = ws;
@@ -181,7 +187,7 @@ int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, co
   const uint32_t* order = sorted ? table_order(d_sizes, nblocks, stream, &ws) : nullptr;
   const int rc = launch_table_kernel(weak != nullptr, static_cast<const uint8_t*>(d_data), len, d_offsets, d_sizes,
                                      nblocks, static_cast<uint8_t*>(d_digests), d_status, weak, order, stream);
-  if (ws) (void)hipFreeAsync(ws, stream);
+  sfi::stream_free(ws, stream);
   return rc;
 }
 
@@ -240,13 +246,16 @@ int batch_with_hashes(const uint8_t* base, uint64_t flen, uint32_t bs, uint32_t 
     return hip_err(hipGetLastError());
   }
   void* state = nullptr;  // every file's SHA-1 state between the two halves of its chain
-  SF_HIP(hipMallocAsync(&state, (size_t)nfiles * 20, s));
+  {
+    const int arc = sfi::stream_alloc(&state, (size_t)nfiles * 20, s);
+    if (arc != SF_OK) return arc;
+  }
   const sf_chain_job first = {dig, nfiles, 1, nbf, state, nullptr};
   const sf_chain_job second = {dig, nfiles, 2, nbf, state, fh};
   int rc = sf_index_device_batch_chained_cols(base, nfiles, flen, bs, 0, cut, dig, nullptr, 0, s);
   if (rc == SF_OK) rc = sf_index_device_batch_chained_cols(base, nfiles, flen, bs, cut, nbf, dig, &first, 1, s);
   if (rc == SF_OK) rc = sf_index_device_batch_chained_cols(nullptr, 0, flen, bs, 0, nbf, nullptr, &second, 1, s);
-  (void)hipFreeAsync(state, s);
+  sfi::stream_free(state, s);
   return rc;
 }
 
@@ -420,7 +429,7 @@ static int sf_index_device_batch_body(const void* d_data, uint64_t len, const sf
   uint8_t* dws = nullptr;
   const size_t ws_bytes = tbl_bytes + fh_bytes;
   if (ws_bytes) {
-    SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&dws), ws_bytes, s));
+    if ((rc = sfi::stream_alloc(reinterpret_cast<void**>(&dws), ws_bytes, s)) != SF_OK) return rc;
     SF_HIP(hipMemcpyAsync(dws, host_ws.data(), ws_bytes, hipMemcpyHostToDevice, s));
   }
   do {
@@ -445,7 +454,7 @@ static int sf_index_device_batch_body(const void* d_data, uint64_t len, const sf
                         d_file_hashes, nullptr, s);
     }
   } while (0);
-  if (dws) (void)hipFreeAsync(dws, s);
+  sfi::stream_free(dws, s);
   return rc;
 }
 

@@ -296,7 +296,8 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
   const auto t0 = std::chrono::steady_clock::now();
   auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-  double t_cut = 0, t_dev = 0;
+  double t_cut = 0, t_dev = 0, t_issue = 0;  // issue: list, buffers and the launch, enqueued
+  double t_ph[4] = {0, 0, 0, 0};  // issue's parts (trace): buffers, list upload, launch, digests back
   std::vector<sf_block_sig> rows_v;
   sf_host_sha1_stream bh;
   sf_host_sha1_begin(&bh);
@@ -424,6 +425,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     // hash the window's chunks: one launch over its bytes in HBM, on st[1]
     // after the window's copies
     const uint64_t n = ends.size();
+    const double i0 = ms();
     if (n) {
       uint8_t *plist = nullptr, *dlist = nullptr, *pdig = nullptr, *ddig = nullptr;
       const uint64_t lbytes = n * (sizeof(uint64_t) + sizeof(uint32_t));
@@ -433,6 +435,8 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
           (rc = res->pin(3 + b, n * 20, reinterpret_cast<void**>(&pdig))) != SF_OK ||
           (rc = res->dev(3 + b, n * 20, reinterpret_cast<void**>(&ddig))) != SF_OK)
         return rc;
+      const double p1 = ms();
+      t_ph[0] += p1 - i0;
       uint64_t* lo = reinterpret_cast<uint64_t*>(plist);
       uint32_t* lz = reinterpret_cast<uint32_t*>(lo + n);
       for (uint64_t j = 0, e = A; j < n; e = ends[j], j++) {
@@ -443,17 +447,23 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
       SF_HIP(hipStreamWaitEvent(st[1], copied.e, 0));
       SF_HIP(hipMemcpyAsync(dlist, plist, lbytes, hipMemcpyHostToDevice, st[1]));
       const uint64_t* d_off = reinterpret_cast<const uint64_t*>(dlist);
+      const double p2 = ms();
+      t_ph[1] += p2 - p1;
       if ((rc = launch_table(dw, B - A, d_off, reinterpret_cast<const uint32_t*>(d_off + n), n, ddig, nullptr,
                              st[1])) != SF_OK)
         return rc;
+      const double p3 = ms();
+      t_ph[2] += p3 - p2;
       SF_HIP(hipMemcpyAsync(pdig, ddig, n * 20, hipMemcpyDeviceToHost, st[1]));
       SF_HIP(hipEventRecord(done_ev[b], st[1]));
+      t_ph[3] += ms() - p3;
       pend[b].on = true;
       pend[b].A = A;
       pend[b].n = n;
       pend[b].plist = plist;
       pend[b].pdig = pdig;
     }
+    t_issue += ms() - i0;
     if (eof) break;
     A = ends.back();
     // the next window is read into the pinned window: this window's copies
@@ -462,12 +472,17 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
     SF_HIP(hipEventSynchronize(copied.e));
     t_dev += ms() - d0;
   }
+  const double h0 = ms();
   if ((rc = harvest(w)) != SF_OK) return rc;  // the last window
+  const double t_last = ms() - h0;
   if (!stamp_of(fd, &after, nullptr)) return SF_EIO;
   if (!same_stamp(before, after)) return SF_EAGAIN;  // written while read: not one version's rows
   if (trace)
-    fprintf(stderr, "sf_index_fd_cut trace: %llu B, %zu blocks, %llu windows: cut+join %.3f, waits %.3f, total %.3f ms\n",
-            (unsigned long long)len, rows_v.size(), (unsigned long long)(w + 1), t_cut, t_dev, ms());
+    fprintf(stderr,
+            "sf_index_fd_cut trace: %llu B, %zu blocks, %llu windows: cut+join %.3f, issue %.3f (buffers %.3f, "
+            "list %.3f, launch %.3f, back %.3f), waits %.3f (last harvest %.3f), total %.3f ms\n",
+            (unsigned long long)len, rows_v.size(), (unsigned long long)(w + 1), t_cut, t_issue, t_ph[0], t_ph[1],
+            t_ph[2], t_ph[3], t_dev, t_last, ms());
   sf_block_sig* out = static_cast<sf_block_sig*>(malloc((rows_v.empty() ? 1 : rows_v.size()) * sizeof(sf_block_sig)));
   if (!out) return SF_ENOMEM;
   if (!rows_v.empty()) memcpy(out, rows_v.data(), rows_v.size() * sizeof(sf_block_sig));

@@ -444,16 +444,16 @@ static int sf_wire_blocks_fd_body(const void* d_digests, const uint32_t* d_sizes
   struct FreeEnds {
     uint64_t* p;
     hipStream_t s;
-    ~FreeEnds() { (void)hipFreeAsync(p, s); }
+    ~FreeEnds() { stream_free(p, s); }
   } free_ends{ends, cs};
   std::vector<uint64_t> cend(nchunks);
   uint64_t* d_cend = nullptr;
-  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cend), nchunks * 8, cs));
+  if ((rc = stream_alloc(reinterpret_cast<void**>(&d_cend), nchunks * 8, cs)) != SF_OK) return rc;
   if ((rc = wire_chunk_ends(ends, n_blocks, per, d_cend, cs)) == SF_OK &&
       (hipMemcpyAsync(cend.data(), d_cend, nchunks * 8, hipMemcpyDeviceToHost, cs) != hipSuccess ||
        hipStreamSynchronize(cs) != hipSuccess))
     rc = SF_ENODEV;
-  (void)hipFreeAsync(d_cend, cs);
+  stream_free(d_cend, cs);
   if (rc != SF_OK) return rc;
   uint64_t cap = 1;
   for (uint64_t k = 0; k < nchunks; k++) cap = std::max(cap, cend[k] - (k ? cend[k - 1] : 0));

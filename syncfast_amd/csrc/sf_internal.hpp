@@ -48,7 +48,7 @@ namespace sfi __attribute__((visibility("hidden"))) {
 // Order = kKnobDefs[] (names, defaults).
 enum Knob {
   K_IO_THREADS, K_INPLACE_MIN_MIB, K_INPLACE_SERIAL, K_FADVISE, K_NO_HOSTREG, K_TABLE_CLASS_BITS, K_TRACE,
-  K_BATCH_FUSED,
+  K_BATCH_FUSED, K_STREAM_POOL,
   K_TEST_INPLACE_FAIL_AT, K_TEST_WIRE_CHUNK, K_TEST_STREAM_STAGE_MIB, K_TEST_LAUNCH_MAX_BLOCKS, K_TEST_TABLE_SORT,
   K_TEST_MULTI_SELF_GATHER, K_TEST_CUT_WINDOW_MIB, K_COUNT
 };
@@ -131,10 +131,15 @@ inline int check_fixed_args(uint64_t len, uint32_t bs) {
 // Launchers of the gfx950 kernels (sf_capi.hip).
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
                  hipStream_t stream, uint32_t* weak = nullptr);
-// Explicit block list (sha1_table_kernel; sorted by length class from 2^17
+// Explicit block list (sha1_table_kernel; sorted by length class from 128
 // blocks).  d_status may be NULL.
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
                  uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr);
+// Stream-ordered scratch (sf_alloc.cpp): allocated, used and freed on one
+// stream, from the library's pool of the stream's device, whose blocks are
+// reused on the freeing stream only.  stream_alloc returns an SF_ code.
+int stream_alloc(void** p, size_t bytes, hipStream_t s);
+void stream_free(void* p, hipStream_t s);
 int launch_wire(const uint8_t* d_digests, uint64_t n, uint32_t bs, uint32_t last, uint8_t* d_out,
                 hipStream_t stream);
 // FILE_BLOCK runs of explicit lists (sf_wire.hip): end offsets of every

@@ -126,7 +126,7 @@ int block_set_build(const void* d_table, const uint8_t* d_present, uint64_t n_ro
   uint64_t cap = 1024;
   while (cap < 2 * n_rows) cap <<= 1;
   sf_block_set* bs = new sf_block_set{static_cast<const uint8_t*>(d_table), n_rows, nullptr, cap - 1};
-  int rc = hip_err(hipMallocAsync(reinterpret_cast<void**>(&bs->slots), cap * sizeof(unsigned long long), s));
+  int rc = stream_alloc(reinterpret_cast<void**>(&bs->slots), cap * sizeof(unsigned long long), s);
   if (rc == SF_OK) rc = hip_err(hipMemsetAsync(bs->slots, 0, cap * sizeof(unsigned long long), s));
   if (rc == SF_OK && n_rows) {
     sfi::clear_stale_error();
@@ -135,7 +135,7 @@ int block_set_build(const void* d_table, const uint8_t* d_present, uint64_t n_ro
     rc = hip_err(hipGetLastError());
   }
   if (rc != SF_OK) {
-    if (bs->slots) (void)hipFreeAsync(bs->slots, s);
+    stream_free(bs->slots, s);
     delete bs;
     return rc;
   }
@@ -174,7 +174,7 @@ int sf_block_set_lookup(const sf_block_set* set, const void* d_query, uint64_t n
 
 int sf_block_set_free(sf_block_set* set, void* stream) {
   if (!set) return SF_OK;
-  const int rc = hip_err(hipFreeAsync(set->slots, as_stream(stream)));
+  const int rc = set->slots ? hip_err(hipFreeAsync(set->slots, as_stream(stream))) : SF_OK;  // stream_free, with its error
   delete set;
   return rc;
 }

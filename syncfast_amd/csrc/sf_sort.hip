@@ -212,10 +212,10 @@ extern "C" int sf_test_table_order_bits(const uint32_t* d_sizes, uint64_t n, uin
   hipStream_t s = static_cast<hipStream_t>(stream);
   void* ws = nullptr;
   const uint32_t kmax = (16u << (mbits < 4 ? 4 : mbits)) - 1u;
-  const hipError_t e = hipMallocAsync(&ws, sfi::class_order_workspace(n, kmax), s);
-  if (e != hipSuccess) return sfi::hip_err(e);
+  const int arc = sfi::stream_alloc(&ws, sfi::class_order_workspace(n, kmax), s);
+  if (arc != SF_OK) return arc;
   const int rc = sfi::class_order(d_sizes, n, mbits, kmax, ws, d_order, s);
-  (void)hipFreeAsync(ws, s);
+  sfi::stream_free(ws, s);
   return rc;
 }
 

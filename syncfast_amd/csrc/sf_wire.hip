@@ -69,8 +69,8 @@ constexpr uint64_t kWireMaxPerLaunch = 1ull << 30;  // messages per launch (grid
 namespace sfi {
 
 // The end offset of every message of the run (inclusive scan of the
-// lengths), in a stream-ordered allocation the caller frees with
-// hipFreeAsync on `s`.
+// lengths), in stream-ordered scratch the caller frees with stream_free on
+// `s`.
 int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_t s) {
   *d_ends = nullptr;
   size_t tmp = 0;
@@ -81,7 +81,10 @@ int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_
   }
   const size_t lb = (n * 8 + 255) & ~(size_t)255;
   uint8_t* ws = nullptr;  // ends first (returned), then lengths and the scan's temporary
-  SF_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws), 2 * lb + tmp + 8, s));
+  {
+    const int arc = stream_alloc(reinterpret_cast<void**>(&ws), 2 * lb + tmp + 8, s);
+    if (arc != SF_OK) return arc;
+  }
   uint64_t* ends = reinterpret_cast<uint64_t*>(ws);
   uint64_t* lens = reinterpret_cast<uint64_t*>(ws + lb);
   int rc = SF_OK;
@@ -100,7 +103,7 @@ int wire_plan(const uint32_t* d_sizes, uint64_t n, uint64_t** d_ends, hipStream_
     rc = SF_ENODEV;
   }
   if (rc != SF_OK) {
-    (void)hipFreeAsync(ws, s);
+    stream_free(ws, s);
     return rc;
   }
   *d_ends = ends;
@@ -159,7 +162,7 @@ int sf_wire_blocks_device(const void* d_digests, const uint32_t* d_sizes, uint64
     rc = sfi::wire_build(static_cast<const uint8_t*>(d_digests), d_sizes, ends, 0, n_blocks, 0,
                          static_cast<uint8_t*>(d_out), s);
   } while (0);
-  (void)hipFreeAsync(ends, s);
+  sfi::stream_free(ends, s);
   return rc;
 }
 

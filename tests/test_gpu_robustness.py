@@ -15,7 +15,12 @@
   opaque zero.
 - A file truncated while indexed (default pread route): no hang or SIGBUS,
   an error or a complete result.
-- index_file sized from a stale stat retries with the need (SF_ENOSPC)."""
+- index_file sized from a stale stat retries with the need (SF_ENOSPC).
+- The library's stream-ordered scratch (sf_alloc.cpp): many-file batches and
+  a one-file fused cut, alternating in one process with small stages, every
+  digest right with the default scratch pool (round 6: the device's default
+  pool, which releases freed blocks at every synchronisation, made such a
+  loop read wrong data through the sort's workspace)."""
 import ctypes
 import os
 import threading
@@ -332,3 +337,52 @@ def test_side_stream_status_is_read_on_that_stream(gpu):
         got = device.index_device_blocks(data, offs[:1], sizes[:1], stream=s)
         s.synchronize()
         assert bytes(got[0].cpu().numpy()) == oracle.sha1(oracle.splitmix_bytes(100, 3))
+
+
+@pytest.mark.parametrize("pool", [1, 2])
+def test_scratch_pool_under_alternating_calls(gpu, knobs, tmp_path, pool):
+    # sf_index_fds_blocks (1 MiB stages on two streams, every stage's list
+    # sorted through the scratch pool) and sf_index_fd_cut (one 2 MiB window,
+    # its list sorted) in turn, 25 times: every row = the oracle's.  Pool 1 is
+    # the default; 2 the same pool with the runtime's cross-stream reuse on
+    # (both kept their blocks and were right in 480 iterations, the pools
+    # that release at every synchronisation wrong in most:
+    # scripts/sort_race_stress.py)
+    import ctypes as C
+    knobs.set("SF_STREAM_POOL", pool)
+    knobs.set("SF_TEST_STREAM_STAGE_MIB", 1)
+    Z = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "build",
+                            "libzpaq_standin.so"))
+    Z.sf_zpaq_standin_ops.restype = C.c_void_p
+    Z.sf_zpaq_standin_ops.argtypes = [C.c_uint, C.c_uint32]
+    ops = Z.sf_zpaq_standin_ops(13, 32768)
+    rng = np.random.default_rng(77)
+    files = []
+    for k, n in enumerate([int(x) for x in rng.integers(1, 300_000, 24)]):
+        p = tmp_path / f"s{k:02d}"
+        d = oracle.splitmix_bytes(n, 5_100 + k)
+        d.tofile(p)
+        z = oracle.zpaq_standin_sizes(d).astype(np.uint32)
+        o = np.concatenate([[0], np.cumsum(z, dtype=np.uint64)[:-1]]).astype(np.uint64)
+        files.append((str(p), o, z, oracle.index_blocks(d, o, z)))
+    big = oracle.splitmix_bytes(2 << 20, 5_199)
+    bp = tmp_path / "big"
+    big.tofile(bp)
+    bz = oracle.zpaq_standin_sizes(big).astype(np.uint32)
+    bwant = oracle.index_blocks(big, np.concatenate([[0], np.cumsum(bz, dtype=np.uint64)[:-1]]).astype(np.uint64), bz)
+    for it in range(25):
+        fds = [os.open(p, os.O_RDONLY) for p, *_ in files]
+        try:
+            rows, first, _bh, st = host.index_fds_blocks(fds, [(o, z) for _p, o, z, _w in files])
+        finally:
+            for fd in fds:
+                os.close(fd)
+        for k, (_p, _o, _z, want) in enumerate(files):
+            assert int(st[k]) == 0 and np.array_equal(rows["sha1"][first[k]:first[k + 1]].reshape(-1, 20), want), \
+                (it, k)
+        fd = os.open(bp, os.O_RDONLY)
+        try:
+            got, _ = host.index_fd_cut(fd, ops, 4)
+        finally:
+            os.close(fd)
+        assert np.array_equal(got["sha1"].reshape(-1, 20), bwant), it

@@ -1,8 +1,9 @@
 """GPU: explicit block lists hashed in order of length (sha1_table_kernel's
 `order`, launch_table's rocprim sort).
 
-The launcher sorts a list of >= 2^17 blocks by compression count, largest
-first, so each wave's 64 blocks are about the same length; every digest must
+The launcher sorts a list of >= 128 blocks (two waves; until round 6 from
+2^17) by compression count, largest first, so each wave's 64 blocks are
+about the same length; every digest must
 still land at its block's own index, bit-identical to the oracle
 (src/index.rs:621-647 restated) and to the list-order launch.
 SF_TEST_TABLE_SORT=1 forces the sorted launch on small lists, SF_TEST_TABLE_SORT=0 the
@@ -144,15 +145,16 @@ def test_sorted_with_launch_split(gpu, knobs):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
 
 
-def test_default_sort_large_cdc_list(gpu, knobs):
-    # >= 2^17 blocks: the launcher sorts by itself; every digest equals the
+@pytest.mark.parametrize("n", [100 * 8192, 300 * 8192, 8415 * 8192, 1 << 30])
+def test_default_sort_cdc_lists(gpu, knobs, n):
+    # from two waves of blocks (128) the launcher sorts by itself: ~100
+    # blocks stay in list order, ~300, configs[0]'s one-window list (~8.4 K)
+    # and a 1 GiB list (~131 K) are sorted; every digest equals the
     # list-order launch and the oracle
     knobs.set("SF_TEST_TABLE_SORT", -1)
-    rng = np.random.default_rng(37_000)
-    n = 1 << 30
+    rng = np.random.default_rng(37_000 + n % 1000)
     data = oracle.splitmix_bytes(n, 47_000)
     offs, sizes = _cdc_like(rng, n)
-    assert offs.size >= 1 << 17
     t = _dev(data, gpu, 5)
     to, tz = torch.from_numpy(offs).to(gpu), torch.from_numpy(sizes.astype(np.int32)).to(gpu)
     got = device.index_device_blocks(t, to, tz).cpu().numpy()
