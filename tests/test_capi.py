@@ -71,6 +71,17 @@ def test_product_kernels_carry_no_retired_ab_forms():
                 assert any(a in t for a in ALLOWED_CONDITIONALS), (fn, t)
 
 
+def test_stream_ordered_scratch_only_from_the_library_pool():
+    """Every stream-ordered allocation of the library goes through
+    stream_alloc (sf_alloc.cpp): the device's default pool, which gives its
+    freed blocks back at every synchronisation, made file calls read wrong
+    data through the sort's workspace ("The scratch pool")."""
+    for fn, src in _product_sources():
+        if fn == "sf_alloc.cpp":
+            continue
+        assert "hipMallocAsync" not in src and "hipMallocFromPoolAsync" not in src, fn
+
+
 def test_environment_read_only_at_load():
     """Knobs are latched once when the library is loaded (sf_knobs.cpp): no
     other translation unit of the shipped library calls getenv, so nothing on
