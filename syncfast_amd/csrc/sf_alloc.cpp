@@ -11,11 +11,12 @@
 // (scripts/sort_race_stress.py, profiles/r06/scratch_pool/) went wrong in
 // 58-60 of 60 iterations in 7 of 8 processes, from the default pool and from
 // a pool of our own with the threshold left at 0 alike, and in 0 of 480 from
-// a pool of our own that keeps its freed blocks (threshold 1 GiB), whether
-// or not the runtime may reuse a block across streams; with no scratch at
-// all (the sort off) 0 of 240.  So the library takes its scratch from a pool
-// of its own per device that keeps up to 1 GiB of freed blocks mapped, and
-// reuses a block only on the stream that freed it.  SF_STREAM_POOL (A/B
+// a pool of our own that keeps its freed blocks (a 1 GiB threshold in that
+// measurement), whether or not the runtime may reuse a block across streams;
+// with no scratch at all (the sort off) 0 of 240.  So the library takes its
+// scratch from a pool of its own per device that keeps every freed block
+// mapped (no threshold: nothing is given back and mapped again), and reuses
+// a block only on the stream that freed it.  SF_STREAM_POOL (A/B
 // knob): 1 that pool (default); 0 hipMallocAsync on the default pool; 2 the
 // pool with cross-stream reuse on; 3 the pool releasing at every
 // synchronisation.
@@ -49,8 +50,10 @@ int stream_device(hipStream_t s, int* dev) {
 
 // The library's pool of device `dev` (created on first use, kept: freeing it
 // from a static destructor could run after the HIP runtime is gone).
-//   mode 1 (shipped): blocks reused on the freeing stream only, up to 1 GiB
-//     of freed blocks kept mapped between calls;
+//   mode 1 (shipped): blocks reused on the freeing stream only, every freed
+//     block kept mapped (the pool holds its peak: the largest scratch is a
+//     sort workspace of at most ~0.6-1 GiB for a 2^27-block launch piece, by
+//     the class-key width);
 //   mode 2: the same pool with the runtime's cross-stream reuse left on;
 //   mode 3: reuse on the freeing stream only, freed blocks released at every
 //     synchronisation (the runtime's default threshold, 0).
@@ -73,7 +76,10 @@ int pool_of(int mode, int dev, hipMemPool_t* out) {
       if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolReuseAllowInternalDependencies, &off);
       if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolReuseFollowEventDependencies, &off);
     }
-    uint64_t keep = mode == 3 ? 0 : 1ull << 30;
+    // keep every freed block (mode 1, 2): a block given back and mapped again
+    // at the same address is what the default pool's users read wrong data
+    // through; a finite threshold would still give back what lies above it
+    uint64_t keep = mode == 3 ? 0 : UINT64_MAX;
     if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
     if (e != hipSuccess) {
       (void)hipMemPoolDestroy(p);
