@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 6: the scratch pool with no release threshold -- the list, file and
+# Round 6: the scratch pool with no release threshold (and, rerun, lists sorted
+# from 65 blocks) -- the list, file and
 # robustness GPU tests, and the alternating-call stress.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

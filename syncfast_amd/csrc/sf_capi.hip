@@ -108,7 +108,7 @@ inline unsigned device_cus() {
   return (unsigned)v;
 }
 
-// Explicit block lists of at least two waves' blocks are hashed in order of
+// Explicit block lists of more than one wave's blocks are hashed in order of
 // length (sha1_table_kernel's `order`): a wave runs as long as its longest
 // block, so 64 blocks of mixed sizes side by side waste most lanes -- a list
 // of content-defined sizes (mean 8 KiB, up to 32 KiB) hashed at 312 GiB/s in
@@ -121,7 +121,7 @@ inline unsigned device_cus() {
 // configs[0]'s one-window list (8,415 blocks): the kernel 1.28 -> 0.69 ms,
 // the sort's three kernels 19 us (profiles/r06/sort_small/).  One wave has
 // nothing to reorder.  SF_TEST_TABLE_SORT=0 / 1 never / always sorts (test hook).
-constexpr uint64_t kTableSortMinBlocks = 128;
+constexpr uint64_t kTableSortMinBlocks = 65;
 inline uint64_t table_sort_min() {
   const int64_t v = knob(K_TEST_TABLE_SORT);
   if (v >= 0) return v ? 1 : ~0ull;

@@ -131,7 +131,7 @@ inline int check_fixed_args(uint64_t len, uint32_t bs) {
 // Launchers of the gfx950 kernels (sf_capi.hip).
 int launch_fixed(const void* d_data, uint64_t len, uint32_t bs, uint64_t nblocks, void* d_digests,
                  hipStream_t stream, uint32_t* weak = nullptr);
-// Explicit block list (sha1_table_kernel; sorted by length class from 128
+// Explicit block list (sha1_table_kernel; sorted by length class from 65
 // blocks).  d_status may be NULL.
 int launch_table(const void* d_data, uint64_t len, const uint64_t* d_offsets, const uint32_t* d_sizes,
                  uint64_t nblocks, void* d_digests, int* d_status, hipStream_t stream, uint32_t* weak = nullptr);

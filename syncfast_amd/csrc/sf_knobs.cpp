@@ -31,7 +31,7 @@ const KnobDef kKnobDefs[K_COUNT] = {
     {"SF_TEST_WIRE_CHUNK", 0},          // K_TEST_WIRE_CHUNK: messages per streamed chunk (0 = 2^18)
     {"SF_TEST_STREAM_STAGE_MIB", 0},    // K_TEST_STREAM_STAGE_MIB: pipeline stage size (0 = 256)
     {"SF_TEST_LAUNCH_MAX_BLOCKS", 0},   // K_TEST_LAUNCH_MAX_BLOCKS: blocks per launch (0 = 2^31)
-    {"SF_TEST_TABLE_SORT", -1},         // K_TEST_TABLE_SORT: -1 auto (>= 128 blocks), 0 never, 1 always
+    {"SF_TEST_TABLE_SORT", -1},         // K_TEST_TABLE_SORT: -1 auto (> 64 blocks), 0 never, 1 always
     {"SF_TEST_MULTI_SELF_GATHER", 0},   // K_TEST_MULTI_SELF_GATHER: one-device multi gather through RCCL (self send/recv)
     {"SF_TEST_CUT_WINDOW_MIB", 0},      // K_TEST_CUT_WINDOW_MIB: sf_index_fd_cut's window (0 = 512 MiB)
 };

@@ -5,7 +5,7 @@ boundaries to the library: every digest and the blocks_hash in list order
 must equal the oracle's restatement of src/index.rs:621-682, across stage
 edges (SF_TEST_STREAM_STAGE_MIB shrinks the ~256 MiB stages), for overlapping and
 empty blocks, blocks larger than a stage, and lists long enough for the
-launcher's length sort (>= 128 blocks in one stage)."""
+launcher's length sort (> 64 blocks in one stage)."""
 import hashlib
 import os
 
@@ -104,7 +104,7 @@ def test_overlapping_empty_and_gapped_blocks(gpu, small_stages):
 
 def test_sorted_launch_inside_a_stage(gpu):
     """2^18 tiny blocks in one stage: the launcher sorts them by length class
-    (>= 128) and every digest still lands at its own row."""
+    (> 64) and every digest still lands at its own row."""
     rng = np.random.default_rng(9)
     n = 1 << 22
     data = oracle.splitmix_bytes(n, 13)

@@ -1,8 +1,8 @@
 """GPU: explicit block lists hashed in order of length (sha1_table_kernel's
 `order`, launch_table's rocprim sort).
 
-The launcher sorts a list of >= 128 blocks (two waves; until round 6 from
-2^17) by compression count, largest first, so each wave's 64 blocks are
+The launcher sorts a list of more than 64 blocks (two waves or more; until
+round 6 from 2^17) by compression count, largest first, so each wave's 64 blocks are
 about the same length; every digest must
 still land at its block's own index, bit-identical to the oracle
 (src/index.rs:621-647 restated) and to the list-order launch.
@@ -145,10 +145,10 @@ def test_sorted_with_launch_split(gpu, knobs):
     assert np.array_equal(got, oracle.index_blocks(data, offs, sizes))
 
 
-@pytest.mark.parametrize("n", [100 * 8192, 300 * 8192, 8415 * 8192, 1 << 30])
+@pytest.mark.parametrize("n", [50 * 8192, 100 * 8192, 300 * 8192, 8415 * 8192, 1 << 30])
 def test_default_sort_cdc_lists(gpu, knobs, n):
-    # from two waves of blocks (128) the launcher sorts by itself: ~100
-    # blocks stay in list order, ~300, configs[0]'s one-window list (~8.4 K)
+    # from two waves of blocks (65) the launcher sorts by itself: ~50 blocks
+    # stay in list order, ~100, ~300, configs[0]'s one-window list (~8.4 K)
     # and a 1 GiB list (~131 K) are sorted; every digest equals the
     # list-order launch and the oracle
     knobs.set("SF_TEST_TABLE_SORT", -1)
