@@ -267,6 +267,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   if (!S_ISREG(mode)) return SF_EINVAL;
   if (expect && !same_stamp(before, *expect)) return SF_EAGAIN;
   const uint64_t len = before.size;
+  const auto ts = std::chrono::steady_clock::now();  // setup (lease, streams, windows): traced apart
   int dev = 0;
   SF_HIP(hipGetDevice(&dev));
   const int64_t wk = knob(K_TEST_CUT_WINDOW_MIB);  // test hook: small windows exercise the window seams
@@ -295,6 +296,7 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   SF_HIP(hipEventCreateWithFlags(&copied.e, hipEventDisableTiming));
   const bool trace = knob(K_TRACE) != 0;  // SF_TRACE=1: phase times on stderr (probe only)
   const auto t0 = std::chrono::steady_clock::now();
+  const double t_setup = std::chrono::duration<double, std::milli>(t0 - ts).count();
   auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   double t_cut = 0, t_dev = 0, t_issue = 0;  // issue: list, buffers and the launch, enqueued
   double t_ph[4] = {0, 0, 0, 0};  // issue's parts (trace): buffers, list upload, launch, digests back
@@ -479,10 +481,11 @@ static int sf_index_fd_cut_body(int fd, const sf_file_stamp* expect, const sf_ch
   if (!same_stamp(before, after)) return SF_EAGAIN;  // written while read: not one version's rows
   if (trace)
     fprintf(stderr,
-            "sf_index_fd_cut trace: %llu B, %zu blocks, %llu windows: cut+join %.3f, issue %.3f (buffers %.3f, "
-            "list %.3f, launch %.3f, back %.3f), waits %.3f (last harvest %.3f), total %.3f ms\n",
-            (unsigned long long)len, rows_v.size(), (unsigned long long)(w + 1), t_cut, t_issue, t_ph[0], t_ph[1],
-            t_ph[2], t_ph[3], t_dev, t_last, ms());
+            "sf_index_fd_cut trace: %llu B, %zu blocks, %llu windows: setup %.3f, cut+join %.3f, issue %.3f "
+            "(buffers %.3f, list %.3f, launch %.3f, back %.3f), waits %.3f (last harvest %.3f), total %.3f ms "
+            "(setup not included)\n",
+            (unsigned long long)len, rows_v.size(), (unsigned long long)(w + 1), t_setup, t_cut, t_issue, t_ph[0],
+            t_ph[1], t_ph[2], t_ph[3], t_dev, t_last, ms());
   sf_block_sig* out = static_cast<sf_block_sig*>(malloc((rows_v.empty() ? 1 : rows_v.size()) * sizeof(sf_block_sig)));
   if (!out) return SF_ENOMEM;
   if (!rows_v.empty()) memcpy(out, rows_v.data(), rows_v.size() * sizeof(sf_block_sig));
