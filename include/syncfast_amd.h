@@ -81,6 +81,15 @@ int sf_release_host_cache(void);
 
 /* --------------------------------------- device-resident hot path ---- */
 
+/* Scratch: calls that need device workspace on `stream` (an explicit list's
+ * length sort, a batch's chain states, wire offsets, block-set slots) take it
+ * stream-ordered from a memory pool of the library's own per device, which
+ * keeps every freed block for later calls (it holds its peak use: at most
+ * ~1 GiB, for a sort of 2^27 blocks) and reuses a block only on the stream
+ * that freed it.  The device's default pool is not used: its blocks, given
+ * back at every synchronisation and mapped again, made calls read wrong data
+ * (DESIGN.md 3.4).  The caller's own allocations are not touched. */
+
 /* Fixed tiling of d_data[0, len) into block_size-byte blocks; writes
  * ceil(len/block_size) digests to d_digests (20 B each).  Replaces the
  * chunk loop of src/index.rs:621-647 for fixed-size blocks.
