@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/p
 for r in 1 2 3 4; do
-  for v in "SF_STREAM_POOL=0" "SF_STREAM_POOL=1" "SF_STREAM_POOL=2" "SF_STREAM_POOL=3" "SF_STREAM_POOL=0 SF_TEST_TABLE_SORT=0"; do
+  for v in "SF_TEST_STREAM_POOL=0" "SF_TEST_STREAM_POOL=1" "SF_TEST_STREAM_POOL=2" "SF_TEST_STREAM_POOL=3" "SF_TEST_STREAM_POOL=0 SF_TEST_TABLE_SORT=0"; do
     env $v SF_TEST_STREAM_STAGE_MIB=1 ITERS=60 timeout -k 10 200 python3 scripts/sort_race_stress.py >> gpurun_out/p/stress.log 2>&1 || exit $?
   done
 done

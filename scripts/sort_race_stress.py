@@ -3,7 +3,7 @@
 digests.  One process alternates, ITERS times, a many-file batch through
 sf_index_fds_blocks (small stages: SF_TEST_STREAM_STAGE_MIB=1, two streams)
 and a 2 MiB file through sf_index_fd_cut, checking every digest against the
-oracle's (computed once).  Settings from the environment (SF_STREAM_POOL,
+oracle's (computed once).  Settings from the environment (SF_TEST_STREAM_POOL,
 SF_TEST_TABLE_SORT, ...); prints one JSON line: iterations with a wrong row,
 per route."""
 import ctypes

@@ -3,7 +3,7 @@
 (tests/test_c_consumer.py::test_c_consumer_default_mode_many_files[4-2])
 gave one wrong digest once explicit lists were sorted from 128 blocks.  The
 same files and command, repeated with the library's scratch from the
-device's default pool (SF_STREAM_POOL=0, hipMallocAsync) and from its own
+device's default pool (SF_TEST_STREAM_POOL=0, hipMallocAsync) and from its own
 pool without cross-stream reuse (1), alternating; per run, the files whose
 rows differ from the oracle and their first wrong blocks."""
 import json
@@ -36,7 +36,7 @@ def main():
     runs = []
     for i in range(int(os.environ.get("ROUNDS", "6"))):
         args = ["-P", "1" if i % 2 else "2", "-K", "2", "-j", "4" if i % 3 else "1"]
-        pair = [("pool0", {"SF_STREAM_POOL": "0"}, args), ("pool1", {"SF_STREAM_POOL": "1"}, args)]
+        pair = [("pool0", {"SF_TEST_STREAM_POOL": "0"}, args), ("pool1", {"SF_TEST_STREAM_POOL": "1"}, args)]
         runs += pair if i % 2 == 0 else pair[::-1]
     for name, env, args in runs:
         r = subprocess.run([exe, "-Z", "-M", "-S", "1"] + args + paths, capture_output=True, text=True, timeout=120,

@@ -16,8 +16,8 @@
 // with no scratch at all (the sort off) 0 of 240.  So the library takes its
 // scratch from a pool of its own per device that keeps every freed block
 // mapped (no threshold: nothing is given back and mapped again), and reuses
-// a block only on the stream that freed it.  SF_STREAM_POOL (A/B
-// knob): 1 that pool (default); 0 hipMallocAsync on the default pool; 2 the
+// a block only on the stream that freed it.  SF_TEST_STREAM_POOL (test
+// hook): 1 that pool (default); 0 hipMallocAsync on the default pool; 2 the
 // pool with cross-stream reuse on; 3 the pool releasing at every
 // synchronisation.
 #include <stdint.h>
@@ -95,7 +95,7 @@ int pool_of(int mode, int dev, hipMemPool_t* out) {
 
 int stream_alloc(void** p, size_t bytes, hipStream_t s) {
   *p = nullptr;
-  const int64_t mode = knob(K_STREAM_POOL);
+  const int64_t mode = knob(K_TEST_STREAM_POOL);
   if (mode == 0) return hip_err(hipMallocAsync(p, bytes, s));
   int dev = 0, rc = stream_device(s, &dev);
   hipMemPool_t pool = nullptr;

@@ -48,9 +48,9 @@ namespace sfi __attribute__((visibility("hidden"))) {
 // Order = kKnobDefs[] (names, defaults).
 enum Knob {
   K_IO_THREADS, K_INPLACE_MIN_MIB, K_INPLACE_SERIAL, K_FADVISE, K_NO_HOSTREG, K_TABLE_CLASS_BITS, K_TRACE,
-  K_BATCH_FUSED, K_STREAM_POOL,
+  K_BATCH_FUSED,
   K_TEST_INPLACE_FAIL_AT, K_TEST_WIRE_CHUNK, K_TEST_STREAM_STAGE_MIB, K_TEST_LAUNCH_MAX_BLOCKS, K_TEST_TABLE_SORT,
-  K_TEST_MULTI_SELF_GATHER, K_TEST_CUT_WINDOW_MIB, K_COUNT
+  K_TEST_MULTI_SELF_GATHER, K_TEST_CUT_WINDOW_MIB, K_TEST_STREAM_POOL, K_COUNT
 };
 struct KnobDef {
   const char* env;

@@ -26,7 +26,6 @@ const KnobDef kKnobDefs[K_COUNT] = {
     {"SF_TABLE_CLASS_BITS", 4},         // K_TABLE_CLASS_BITS: mantissa bits of the length class (<= 4: 8-bit key)
     {"SF_TRACE", 0},                    // K_TRACE: sf_index_files / sf_index_fds_blocks phase times on stderr
     {"SF_BATCH_FUSED", 1},              // K_BATCH_FUSED: sf_index_device_batch's two halves (0: blocks, then chains)
-    {"SF_STREAM_POOL", 1},              // K_STREAM_POOL: scratch from the library's own pool (0: the device's default pool)
     {"SF_TEST_INPLACE_FAIL_AT", -1},    // K_TEST_INPLACE_FAIL_AT: region k "fails" to page-lock
     {"SF_TEST_WIRE_CHUNK", 0},          // K_TEST_WIRE_CHUNK: messages per streamed chunk (0 = 2^18)
     {"SF_TEST_STREAM_STAGE_MIB", 0},    // K_TEST_STREAM_STAGE_MIB: pipeline stage size (0 = 256)
@@ -34,6 +33,7 @@ const KnobDef kKnobDefs[K_COUNT] = {
     {"SF_TEST_TABLE_SORT", -1},         // K_TEST_TABLE_SORT: -1 auto (> 64 blocks), 0 never, 1 always
     {"SF_TEST_MULTI_SELF_GATHER", 0},   // K_TEST_MULTI_SELF_GATHER: one-device multi gather through RCCL (self send/recv)
     {"SF_TEST_CUT_WINDOW_MIB", 0},      // K_TEST_CUT_WINDOW_MIB: sf_index_fd_cut's window (0 = 512 MiB)
+    {"SF_TEST_STREAM_POOL", 1},         // K_TEST_STREAM_POOL: scratch pool (1 own, keeps blocks; 0 / 3 known wrong)
 };
 
 std::atomic<int64_t> g_knob[K_COUNT];

@@ -349,7 +349,7 @@ def test_scratch_pool_under_alternating_calls(gpu, knobs, tmp_path, pool):
     # that release at every synchronisation wrong in most:
     # scripts/sort_race_stress.py)
     import ctypes as C
-    knobs.set("SF_STREAM_POOL", pool)
+    knobs.set("SF_TEST_STREAM_POOL", pool)
     knobs.set("SF_TEST_STREAM_STAGE_MIB", 1)
     Z = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "build",
                             "libzpaq_standin.so"))
