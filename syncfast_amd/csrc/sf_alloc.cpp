@@ -76,9 +76,9 @@ int pool_of(int mode, int dev, hipMemPool_t* out) {
       if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolReuseAllowInternalDependencies, &off);
       if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolReuseFollowEventDependencies, &off);
     }
-    // keep every freed block (mode 1, 2): a block given back and mapped again
-    // at the same address is what the default pool's users read wrong data
-    // through; a finite threshold would still give back what lies above it
+    // keep every freed block (mode 1, 2): the measurement ties the wrong data
+    // to pools that give freed blocks back at synchronisation points, and a
+    // finite threshold would still give back what lies above it
     uint64_t keep = mode == 3 ? 0 : UINT64_MAX;
     if (e == hipSuccess) e = hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
     if (e != hipSuccess) {
